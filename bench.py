@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark: batched RNEA (fr3 7-DOF) evals/s on MI355X, BASELINE.json's metric.
+
+One step = one launch of the RNEA kernel over one batch of B configurations
+(default B = 2^20 per GPU, fp32, SoA, inputs already resident in HBM).  The input
+sets rotate through >1 GiB of device memory so the 256 MiB Infinity Cache cannot
+serve them.  N > 1: one process per GPU (torch.distributed.run), the model is loaded
+on rank 0 and broadcast as a blob over RCCL, every rank evaluates its own batch
+(weak scaling, no data-path collective), timing is max over ranks.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §5 for how roofline/cpu_baseline are
+derived; profiles/ holds the rocprofv3 summaries these numbers are checked against.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "rigidbody-rs_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from rigidbody_amd import chains, ffi  # noqa: E402
+
+HBM_PEAK = 8.0e12  # B/s, MI355X spec (/opt/skills/guides/MI355X_MICROARCH.md)
+DT = {"f32": torch.float32, "f64": torch.float64}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="configurations per GPU per step")
+    ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--kernel", choices=["rnea", "fd"], default="rnea")
+    ap.add_argument("--dof", type=int, default=7, help="7 = FR3; other values = synthetic z-chain")
+    ap.add_argument("--rotate-gib", type=float, default=1.25, help="device memory the input sets span")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work budget of the baseline sample")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / forward-dynamics side lines")
+    return ap.parse_args()
+
+
+def init_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def load_model(world, rank, dof):
+    """Rank 0 parses the URDF; the packed fp64 model blob is broadcast over RCCL."""
+    import torch.distributed as dist
+
+    if rank == 0:
+        mb = ffi.Multibody.new() if dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(dof))
+        blob = torch.as_tensor(mb.blob(), device="cuda")
+        size = torch.tensor([blob.numel()], device="cuda", dtype=torch.int64)
+    else:
+        size = torch.zeros(1, device="cuda", dtype=torch.int64)
+    if world > 1:
+        dist.broadcast(size, 0)
+        if rank != 0:
+            blob = torch.empty(int(size.item()), device="cuda", dtype=torch.float64)
+        dist.broadcast(blob, 0)
+        if rank != 0:
+            mb = ffi.Multibody.from_blob(blob.cpu().numpy())
+    mb.upload()
+    return mb
+
+
+def make_sets(mb, B, dtype, kernel, nsets, seed):
+    lim = mb.limits()
+    kinds = ("q", "qd", "qdd") if kernel == "rnea" else ("q", "qd", "tau")
+    sets = []
+    for s in range(nsets):
+        ins = []
+        for k, kind in enumerate(kinds):
+            lo, hi = chains.input_ranges(lim, kind)
+            t = torch.empty((mb.n, B), dtype=dtype, device="cuda")
+            ffi.fill_uniform(t, lo, hi, seed + 1000 * s + k)
+            ins.append(t)
+        out = torch.empty((mb.n, B), dtype=dtype, device="cuda")
+        sets.append((ins, out))
+    torch.cuda.synchronize()
+    return sets
+
+
+def run_timed(mb, sets, kernel, dtype, steps, warmup, world):
+    """Warmup, then exactly `steps` launches bracketed by barrier + synchronize.
+    Per-launch hipEvent pairs on the launch stream give the kernel's device time."""
+    lib = ffi.lib()
+    suffix = "f32" if dtype == torch.float32 else "f64"
+    fn = getattr(lib, f"multibody_{'rnea' if kernel == 'rnea' else 'fd'}_batch_{suffix}")
+    stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    B = sets[0][1].shape[1]
+    args = [(mb.handle, ins[0].data_ptr(), ins[1].data_ptr(), ins[2].data_ptr(), out.data_ptr(), B, B, sp)
+            for ins, out in sets]
+    ns = len(args)
+    for i in range(warmup):
+        rc = fn(*args[i % ns])
+        if rc:
+            raise RuntimeError(ffi.last_error())
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        rc = fn(*args[i % ns])
+        ev[i][1].record(stream)
+        if rc:
+            raise RuntimeError(ffi.last_error())
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        torch.distributed.barrier()
+    wall = t1 - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    return wall, float(np.mean(kern_ms)), float(np.median(kern_ms))
+
+
+def cpu_baseline(n, B_sample_hint, kernel, cpu_seconds):
+    """fp64 CPU restatement (oracle/, kind "port") timed on this host's cores."""
+    from oracle import oracle, urdf_model
+
+    oracle.build()
+    xml = chains.fr3_urdf_text() if n == 7 else chains.synthetic_chain_urdf(n)
+    raw = urdf_model.model_raw_from_urdf(xml)
+    om = oracle.Model(raw)
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(16, cores))  # the GPU box's CPU share is 16
+    mbl = ([l["lower"] for l in raw["limits"]], [l["upper"] for l in raw["limits"]],
+           [l["velocity"] for l in raw["limits"]], [l["effort"] for l in raw["limits"]])
+    kinds = ("q", "qd", "qdd") if kernel == "rnea" else ("q", "qd", "tau")
+
+    def inputs(B):
+        return [chains.host_uniform(n, B, *chains.input_ranges(mbl, kind), chains.SEED + k)
+                for k, kind in enumerate(kinds)]
+
+    call = om.rnea_batch if kernel == "rnea" else om.fd_batch
+    cal = inputs(20000)
+    t = time.perf_counter()
+    call(*cal, nthreads=1)
+    rate1 = 20000 / (time.perf_counter() - t)
+    sample = int(min(max(rate1 * cpu_seconds, 1e5), 5e7))
+    x = inputs(sample)
+    t = time.perf_counter()
+    call(*x, nthreads=cores)
+    dt = time.perf_counter() - t
+    return {"value": sample / dt, "unit": "evals/s", "cores": cores, "kind": "port",
+            "sample": f"{sample} fr3 configs (same distributions/seed as the GPU run), fp64 oracle "
+                      f"{kernel} over {cores} OpenMP threads, {dt:.2f} s wall; single-thread {rate1:.3g} evals/s"}
+
+
+def load_traffic(workload):
+    path = os.path.join(REPO, "profiles", f"traffic_{workload}.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    a = parse()
+    world, rank, local = init_dist()
+    n = a.dof
+    dtype = DT[a.dtype]
+    esize = 4 if a.dtype == "f32" else 8
+    mb = load_model(world, rank, n)
+    per_set = 4 * n * a.batch * esize
+    nsets = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / per_set)))
+    sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED + 7919 * rank)
+    wall, kern_avg_ms, kern_med_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world)
+    if world > 1:
+        t = torch.tensor([wall], device="cuda", dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        wall = t.item()
+        k = torch.tensor([kern_avg_ms], device="cuda", dtype=torch.float64)
+        torch.distributed.all_reduce(k, op=torch.distributed.ReduceOp.MAX)
+        kern_avg_ms = k.item()
+    evals = world * a.batch * a.steps
+    value = evals / wall
+    bytes_per_eval = 4 * n * esize  # q, qd, qdd|tau read + tau|qdd written
+    achieved = bytes_per_eval * a.batch / (kern_avg_ms * 1e-3)
+    workload = f"{'rnea' if a.kernel == 'rnea' else 'fd'}_{'fr3' if n == 7 else f'chain{n}'}_{a.dtype}_b{a.batch}"
+    traffic = load_traffic(workload)
+    line = {
+        "metric": "RNEA evals/sec (fr3 7-DOF, batch 2^20) at 1/2/4/8 MI355X; % HBM roofline",
+        "value": value,
+        "unit": "evals/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": wall / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": a.dtype,
+        "data": "synthetic (device splitmix64, SURVEY.md §8(d) distributions, seed 20250224)",
+        "config": {"workload": workload, "kernel": a.kernel, "model": "fr3 7-DOF" if n == 7 else f"chain{n}",
+                   "batch_per_gpu": a.batch, "global_batch": a.batch * world, "dof": n,
+                   "parallelism": f"dp{world} (independent shards, RCCL model broadcast)",
+                   "input_sets": nsets, "rotated_bytes": nsets * per_set},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK,
+                     "traffic": traffic["bytes_per_launch"] if traffic else None,
+                     "bytes_per_eval": bytes_per_eval, "kernel_ms_avg": kern_avg_ms, "kernel_ms_median": kern_med_ms},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(n, a.batch, a.kernel, a.cpu_seconds)
+    if rank == 0 and not a.no_secondary and world == 1:
+        sec = {}
+        for kern, dt in (("rnea", "f64"), ("fd", "f32"), ("fd", "f64")):
+            ds = DT[dt]
+            es = 4 if dt == "f32" else 8
+            ps = 4 * n * a.batch * es
+            ns = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / ps)))
+            del sets
+            torch.cuda.empty_cache()
+            sets = make_sets(mb, a.batch, ds, kern, ns, chains.SEED + 31)
+            w, km, _ = run_timed(mb, sets, kern, ds, max(20, a.steps // 4), 5, 1)
+            sec[f"{kern}_{dt}"] = {"evals_per_s": a.batch * max(20, a.steps // 4) / w, "kernel_ms_avg": km,
+                                   "hbm_frac": 4 * n * es * a.batch / (km * 1e-3) / HBM_PEAK}
+        line["secondary"] = sec
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+/*
+ * rigidbody_batch.h -- batched GPU extension of the rigidbody_bindings C ABI.
+ *
+ * The reference exposes one configuration per call (rigidbody_bindings/src/lib.rs:15-70).
+ * These entry points evaluate B configurations per call on one MI355X (gfx950) with
+ * hand-written HIP kernels.  They replace, for a batch, a loop of the reference calls:
+ *
+ *   multibody_rnea_batch_*     <- multibody_rnea      (lib.rs:15-30, multibody.rs:111-153)
+ *   multibody_fd_batch_*       <- no reference entry point: forward dynamics defined as
+ *                                 qdd = sym(H)^-1 (tau - rnea(q,qd,0)) with H from
+ *                                 multibody_crba (multibody.rs:155-174), computed by the
+ *                                 Articulated-Body Algorithm
+ *   multibody_crba_batch_*     <- multibody_crba      (lib.rs:32-43)
+ *   multibody_fwd_kin_batch_*  <- multibody_fwd_kin   (lib.rs:46-57)
+ *   multibody_jac_batch_*      <- multibody_jac       (lib.rs:60-70)
+ *
+ * Layout: structure of arrays.  Joint j of configuration b lives at x[j * ld + b]
+ * (ld >= batch, the leading dimension).  Matrix outputs store element e of each
+ * configuration at out[e * ld + b], with e following the single-call ABI's
+ * column-major order (crba: e = row + n*col; jac: e = row + 6*col; fwd_kin: e = 0..2).
+ *
+ * Pointers: the plain entry points take DEVICE pointers (hipMalloc'd memory on the
+ * current HIP device) and enqueue asynchronously on `stream` (a hipStream_t; NULL =
+ * the null stream).  The *_host variants take host pointers and block until done.
+ *
+ * Return value: RB_OK (0) or an rb_status error code; rb_last_error() gives a
+ * thread-local message.  No entry point aborts the process.
+ *
+ * Reentrancy: a Multibody is immutable after construction; calls on one handle
+ * from several threads are safe (device model constants are uploaded once per
+ * device under a lock; the single-config ABI uses thread-local staging).
+ */
+#ifndef RIGIDBODY_BATCH_H
+#define RIGIDBODY_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rigidbody.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    RB_OK = 0,
+    RB_ERR_NULL = 1,        /* NULL handle or pointer */
+    RB_ERR_ARG = 2,         /* bad size / leading dimension / buffer length */
+    RB_ERR_HIP = 3,         /* HIP runtime error (message in rb_last_error) */
+    RB_ERR_URDF = 4,        /* URDF could not be read or parsed */
+    RB_ERR_DOF = 5,         /* DOF outside the compiled kernel set */
+    RB_ERR_UNSUPPORTED = 6, /* model feature outside the reference's semantics */
+    RB_ERR_NUMERIC = 7      /* singular articulated inertia in FD */
+} rb_status;
+
+/* ---- model construction ------------------------------------------------------- */
+/* Multibody::from_urdf (multibody.rs:65-77) on a file / an in-memory string.  Any
+ * number of revolute joints for which a kernel is compiled (multibody_supported_dofs). */
+Multibody *multibody_new_from_urdf(const char *path);
+Multibody *multibody_new_from_urdf_string(const char *xml, size_t len);
+/* Packed fp64 model (bit-exact), for broadcasting one model to every rank (RCCL). */
+int64_t multibody_blob_size(const Multibody *mb);                 /* in doubles */
+int multibody_export_blob(const Multibody *mb, double *out, int64_t len);
+Multibody *multibody_new_from_blob(const double *blob, int64_t len);
+
+int multibody_dof(const Multibody *mb);
+/* Total moving mass (sum of link masses). */
+double multibody_total_mass(const Multibody *mb);
+/* Joint limits parsed from the URDF (NaN where absent); arrays of multibody_dof. */
+int multibody_limits(const Multibody *mb, double *lower, double *upper,
+                     double *velocity, double *effort);
+/* Writes up to `cap` DOF values the kernels are compiled for; returns their count. */
+int multibody_supported_dofs(int *out, int cap);
+
+/* Uploads the model constants to the current HIP device now (otherwise done lazily on
+ * the first batched call); call before capturing batched calls into a hipGraph. */
+int multibody_upload(const Multibody *mb);
+
+void multibody_result_free(double *p);
+const char *rb_last_error(void);
+const char *rb_version(void);
+
+/* ---- batched device-pointer entry points (asynchronous on `stream`) ------------ */
+int multibody_rnea_batch_f32(const Multibody *mb, const float *q, const float *qd,
+                             const float *qdd, float *tau, int64_t batch, int64_t ld,
+                             void *stream);
+int multibody_rnea_batch_f64(const Multibody *mb, const double *q, const double *qd,
+                             const double *qdd, double *tau, int64_t batch, int64_t ld,
+                             void *stream);
+int multibody_fd_batch_f32(const Multibody *mb, const float *q, const float *qd,
+                           const float *tau, float *qdd, int64_t batch, int64_t ld,
+                           void *stream);
+int multibody_fd_batch_f64(const Multibody *mb, const double *q, const double *qd,
+                           const double *tau, double *qdd, int64_t batch, int64_t ld,
+                           void *stream);
+int multibody_crba_batch_f32(const Multibody *mb, const float *q, float *H,
+                             int64_t batch, int64_t ld, void *stream);
+int multibody_crba_batch_f64(const Multibody *mb, const double *q, double *H,
+                             int64_t batch, int64_t ld, void *stream);
+int multibody_fwd_kin_batch_f64(const Multibody *mb, const double *q, double *pos,
+                                int64_t batch, int64_t ld, void *stream);
+int multibody_jac_batch_f64(const Multibody *mb, const double *q, double *J,
+                            int64_t batch, int64_t ld, void *stream);
+
+/* ---- batched host-pointer entry points (blocking) ------------------------------ */
+int multibody_rnea_batch_host_f64(const Multibody *mb, const double *q, const double *qd,
+                                  const double *qdd, double *tau, int64_t batch);
+int multibody_fd_batch_host_f64(const Multibody *mb, const double *q, const double *qd,
+                                const double *tau, double *qdd, int64_t batch);
+
+/* ---- synthetic inputs, generated on device ------------------------------------- */
+/* x[j*ld + b] = lo[j] + (hi[j]-lo[j]) * u(seed, j, b), u = splitmix64 -> [0,1) with
+ * 53-bit (f64) / 24-bit (f32) mantissa; lo/hi are host arrays of n_rows. */
+int rb_fill_uniform_f32(float *x, int n_rows, int64_t batch, int64_t ld, const double *lo,
+                        const double *hi, uint64_t seed, void *stream);
+int rb_fill_uniform_f64(double *x, int n_rows, int64_t batch, int64_t ld, const double *lo,
+                        const double *hi, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RIGIDBODY_BATCH_H */

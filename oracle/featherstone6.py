@@ -1,0 +1,183 @@
+"""TEST INFRASTRUCTURE ONLY -- independent 6x6 cross-check of the C restatement.
+
+A second, structurally different formulation of the same dynamics, used to validate
+oracle.c (which follows the reference's quaternion/isometry code path):
+
+* rotations as 3x3 matrices built directly (Rz(y)Ry(p)Rx(r) and Rodrigues for the
+  joint), never through quaternions or the axis-angle round trip of joint.rs:57-64;
+* Featherstone 6x6 Pluecker matrices in the reference's [rot; lin] ordering
+  (spatial.rs:137-149): motion transform B_X_A = [[E, 0], [-E r^, E]]
+  (spatial.rs:32-47 form, E = parent->child rotation, r = child origin in parent),
+  force transforms as its transpose, spatial inertia in the `to_matrix6` form
+  (inertia.rs:53-70), motion/force cross-product matrices (Featherstone 2.31/2.32);
+* RNEA and CRBA as Featherstone Tables 5.1 / 6.2, and the Articulated-Body
+  Algorithm (Table 7.1) as an independent forward-dynamics check of the oracle's
+  CRBA-solve definition.
+
+Like the reference it injects joint motion about local z (multibody.rs:130-138)
+and applies gravity as a +9.81 z base acceleration (multibody.rs:117-120).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+G = 9.81
+S = np.array([0.0, 0.0, 1.0, 0.0, 0.0, 0.0])
+
+
+def skew(v):
+    return np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
+
+
+def rpy_matrix(r, p, y):
+    cr, sr, cp, sp, cy, sy = np.cos(r), np.sin(r), np.cos(p), np.sin(p), np.cos(y), np.sin(y)
+    Rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    Ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def axis_angle_matrix(a, q):
+    a = np.asarray(a, float) / np.linalg.norm(a)
+    K = skew(a)
+    return np.eye(3) + np.sin(q) * K + (1 - np.cos(q)) * (K @ K)
+
+
+def xmotion(E, r):
+    """B_X_A (spatial.rs:32-47 form) for E = rotation A->B coords, r = B origin in A."""
+    X = np.zeros((6, 6))
+    X[:3, :3] = E
+    X[3:, 3:] = E
+    X[3:, :3] = -E @ skew(r)
+    return X
+
+
+def inertia6(mass, com, icom):
+    """Inertia::from_com (inertia.rs:21-35) then to_matrix6 (inertia.rs:53-70)."""
+    C = skew(com)
+    Io = icom + mass * C @ C.T
+    M = np.zeros((6, 6))
+    M[:3, :3] = Io
+    M[:3, 3:] = mass * C
+    M[3:, :3] = mass * C.T
+    M[3:, 3:] = mass * np.eye(3)
+    return M
+
+
+def crm(v):
+    M = np.zeros((6, 6))
+    M[:3, :3] = skew(v[:3])
+    M[3:, 3:] = skew(v[:3])
+    M[3:, :3] = skew(v[3:])
+    return M
+
+
+def crf(v):
+    return -crm(v).T
+
+
+class Model6:
+    def __init__(self, raw):
+        self.n = int(raw["n"])
+        self.Rp = [rpy_matrix(*raw["rpy"][i]) for i in range(self.n)]
+        self.p = [np.asarray(raw["xyz"][i], float) for i in range(self.n)]
+        self.axis = [np.asarray(raw["axis"][i], float) for i in range(self.n)]
+        self.I = []
+        for i in range(self.n):
+            j = raw["inertia6"][i]
+            ic = np.array([[j[0], j[1], j[2]], [j[1], j[3], j[4]], [j[2], j[4], j[5]]])
+            self.I.append(inertia6(raw["mass"][i], np.asarray(raw["com"][i], float), ic))
+
+    def poses(self, q):
+        return [(self.Rp[i] @ axis_angle_matrix(self.axis[i], q[i]), self.p[i]) for i in range(self.n)]
+
+    def xforms(self, q):
+        return [xmotion(R.T, p) for R, p in self.poses(q)]
+
+    def rnea(self, q, qd, qdd):
+        X = self.xforms(q)
+        v = np.zeros(6)
+        a = np.array([0, 0, 0, 0, 0, G], float)
+        f = []
+        for i in range(self.n):
+            vJ = S * qd[i]
+            v = X[i] @ v + vJ
+            a = X[i] @ a + S * qdd[i] + crm(v) @ vJ
+            f.append(self.I[i] @ a + crf(v) @ self.I[i] @ v)
+        tau = np.zeros(self.n)
+        for i in range(self.n - 1, -1, -1):
+            tau[i] = S @ f[i]
+            if i > 0:
+                f[i - 1] = f[i - 1] + X[i].T @ f[i]
+        return tau
+
+    def crba(self, q):
+        X = self.xforms(q)
+        Ic = [M.copy() for M in self.I]
+        for i in range(self.n - 1, 0, -1):
+            Ic[i - 1] = Ic[i - 1] + X[i].T @ Ic[i] @ X[i]
+        H = np.zeros((self.n, self.n))
+        for i in range(self.n):
+            F = Ic[i] @ S
+            H[i, i] = S @ F
+            j = i
+            while j > 0:
+                F = X[j].T @ F
+                j -= 1
+                H[i, j] = H[j, i] = S @ F
+        return H
+
+    def aba(self, q, qd, tau):
+        n = self.n
+        X = self.xforms(q)
+        v, c, IA, pA = [None] * n, [None] * n, [None] * n, [None] * n
+        vp = np.zeros(6)
+        for i in range(n):
+            vJ = S * qd[i]
+            v[i] = X[i] @ vp + vJ
+            c[i] = crm(v[i]) @ vJ
+            IA[i] = self.I[i].copy()
+            pA[i] = crf(v[i]) @ self.I[i] @ v[i]
+            vp = v[i]
+        U, D, u = [None] * n, np.zeros(n), np.zeros(n)
+        for i in range(n - 1, -1, -1):
+            U[i] = IA[i] @ S
+            D[i] = S @ U[i]
+            u[i] = tau[i] - S @ pA[i]
+            if i > 0:
+                Ia = IA[i] - np.outer(U[i], U[i]) / D[i]
+                pa = pA[i] + Ia @ c[i] + U[i] * u[i] / D[i]
+                IA[i - 1] = IA[i - 1] + X[i].T @ Ia @ X[i]
+                pA[i - 1] = pA[i - 1] + X[i].T @ pa
+        qdd = np.zeros(n)
+        ap = np.array([0, 0, 0, 0, 0, G], float)
+        for i in range(n):
+            a = X[i] @ ap + c[i]
+            qdd[i] = (u[i] - U[i] @ a) / D[i]
+            a = a + S * qdd[i]
+            ap = a
+        return qdd
+
+    def fwd_kin(self, q):
+        R, p = np.eye(3), np.zeros(3)
+        for Ri, pi in self.poses(q):
+            p = p + R @ pi
+            R = R @ Ri
+        return p
+
+    def jac(self, q):
+        """Body Jacobian of the last link, rows [lin; rot] (multibody.rs:95-108)."""
+        poses = self.poses(q)
+        n = self.n
+        J = np.zeros((6, n))
+        R, p = np.eye(3), np.zeros(3)  # pose of the last frame in frame i (built backwards)
+        for i in range(n - 1, -1, -1):
+            # joint-i axis z in frame i, expressed at/in the last frame: X(R^T, p) applied to S
+            X = xmotion(R.T, p)
+            sv = X @ S
+            J[:3, i] = sv[3:]
+            J[3:, i] = sv[:3]
+            Ri, pi = poses[i]
+            p = pi + Ri @ p
+            R = Ri @ R
+        return J

@@ -1,0 +1,107 @@
+// artinertia.hip.hpp -- 6x6 spatial / articulated inertia in 3x3 block form (device).
+// Shared by aba.hip (articulated inertia) and crba.hip (composite inertia).
+#pragma once
+
+#include "spatial.hip.hpp"
+
+namespace rbamd {
+namespace dev {
+
+// ------------------------------------------------------ articulated-body (ABA) helpers
+// Articulated inertia in block form [[A, B], [B^T, M]] acting on (rot, lin).
+template <typename T>
+struct ArtI {
+    S3<T> A;
+    M3<T> B;
+    S3<T> M;
+};
+
+template <typename T>
+__device__ __forceinline__ ArtI<T> rigid_inertia(const Link<T> &L) {
+    // I_o, [h]x, m*1  (Inertia::to_matrix6 form, inertia.rs:53-70)
+    ArtI<T> I;
+    I.A = L.Io;
+    I.B = M3<T>{{T(0), -L.h.z, L.h.y, L.h.z, T(0), -L.h.x, -L.h.y, L.h.x, T(0)}};
+    I.M = S3<T>{L.m, T(0), T(0), L.m, T(0), L.m};
+    return I;
+}
+
+// E S E^T for symmetric S
+template <typename T>
+__device__ __forceinline__ S3<T> rot_sym(const M3<T> &E, const S3<T> &S) {
+    const T s[9] = {S.xx, S.xy, S.xz, S.xy, S.yy, S.yz, S.xz, S.yz, S.zz};
+    T t[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            t[3 * r + c] = fmadd(E.m[3 * r + 0], s[c], fmadd(E.m[3 * r + 1], s[3 + c], E.m[3 * r + 2] * s[6 + c]));
+    auto e = [&](int r, int c) {
+        return fmadd(t[3 * r + 0], E.m[3 * c + 0], fmadd(t[3 * r + 1], E.m[3 * c + 1], t[3 * r + 2] * E.m[3 * c + 2]));
+    };
+    return S3<T>{e(0, 0), e(0, 1), e(0, 2), e(1, 1), e(1, 2), e(2, 2)};
+}
+
+// E B E^T for general B
+template <typename T>
+__device__ __forceinline__ M3<T> rot_full(const M3<T> &E, const M3<T> &Bm) {
+    T t[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            t[3 * r + c] = fmadd(E.m[3 * r + 0], Bm.m[c], fmadd(E.m[3 * r + 1], Bm.m[3 + c], E.m[3 * r + 2] * Bm.m[6 + c]));
+    M3<T> o;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            o.m[3 * r + c] = fmadd(t[3 * r + 0], E.m[3 * c + 0], fmadd(t[3 * r + 1], E.m[3 * c + 1], t[3 * r + 2] * E.m[3 * c + 2]));
+    return o;
+}
+
+// X^T Ia X for the child->parent transform (E, p): rotate blocks, then shift by
+// P = [p]x:  B'' = B' + P M',  A'' = A' + P B'^T + B'' P^T,  M'' = M'.
+template <typename T>
+__device__ __forceinline__ ArtI<T> to_parent(const M3<T> &E, const V3<T> &p, const ArtI<T> &I) {
+    const S3<T> A1 = rot_sym(E, I.A);
+    const M3<T> B1 = rot_full(E, I.B);
+    const S3<T> M1 = rot_sym(E, I.M);
+    const T m[9] = {M1.xx, M1.xy, M1.xz, M1.xy, M1.yy, M1.yz, M1.xz, M1.yz, M1.zz};
+    M3<T> B2;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        // rows of P = [[0,-pz,py],[pz,0,-px],[-py,px,0]]
+        B2.m[0 + c] = fmadd(-p.z, m[3 + c], fmadd(p.y, m[6 + c], B1.m[0 + c]));
+        B2.m[3 + c] = fmadd(p.z, m[0 + c], fmadd(-p.x, m[6 + c], B1.m[3 + c]));
+        B2.m[6 + c] = fmadd(-p.y, m[0 + c], fmadd(p.x, m[3 + c], B1.m[6 + c]));
+    }
+    const T P[9] = {T(0), -p.z, p.y, p.z, T(0), -p.x, -p.y, p.x, T(0)};
+    // (P B1^T)[r][c] = sum_k P[r][k] B1[c][k];  (B2 P^T)[r][c] = sum_k B2[r][k] P[c][k]
+    auto a = [&](int r, int c, T base) {
+        T s = base;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s = fmadd(P[3 * r + k], B1.m[3 * c + k], s);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) s = fmadd(B2.m[3 * r + k], P[3 * c + k], s);
+        return s;
+    };
+    ArtI<T> o;
+    o.A = S3<T>{a(0, 0, A1.xx), a(0, 1, A1.xy), a(0, 2, A1.xz), a(1, 1, A1.yy), a(1, 2, A1.yz), a(2, 2, A1.zz)};
+    o.B = B2;
+    o.M = M1;
+    return o;
+}
+
+template <typename T>
+__device__ __forceinline__ void add_rigid(ArtI<T> &I, const Link<T> &L) {
+    I.A.xx += L.Io.xx; I.A.xy += L.Io.xy; I.A.xz += L.Io.xz;
+    I.A.yy += L.Io.yy; I.A.yz += L.Io.yz; I.A.zz += L.Io.zz;
+    I.B.m[1] -= L.h.z; I.B.m[2] += L.h.y;
+    I.B.m[3] += L.h.z; I.B.m[5] -= L.h.x;
+    I.B.m[6] -= L.h.y; I.B.m[7] += L.h.x;
+    I.M.xx += L.m; I.M.yy += L.m; I.M.zz += L.m;
+}
+
+}  // namespace dev
+}  // namespace rbamd

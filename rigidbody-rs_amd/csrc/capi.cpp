@@ -1,0 +1,561 @@
+// capi.cpp -- the extern "C" boundary (include/rigidbody.h, include/rigidbody_batch.h).
+//
+// Drop-in for the Rust cdylib rigidbody_bindings (rigidbody_bindings/src/lib.rs:8-78):
+// same six symbols and result layouts, plus batched device-pointer entry points.
+// Every compute entry point runs a HIP kernel on the current device; there is no CPU
+// compute path in this library (model loading and argument checks only).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/rigidbody_batch.h"
+#include "kernels.hpp"
+#include "model.hpp"
+
+#include "fr3_embedded.inc"  // kFr3Urdf: compact FR3 description (tools/gen_fixtures.py)
+
+#define RB_VERSION "rigidbody-rs_amd 0.1.0 (gfx950)"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_err(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_err(hipError_t e, const char *where) {
+    return set_err(RB_ERR_HIP, std::string(where) + ": " + hipGetErrorName(e) + " (" +
+                                   hipGetErrorString(e) + ")");
+}
+
+bool env_flag(const char *name, bool dflt) {
+    const char *v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    return !(v[0] == '0' || v[0] == 'n' || v[0] == 'N' || v[0] == 'f' || v[0] == 'F');
+}
+
+// fp32 kernels use the hardware sin/cos (v_sin_f32 / v_cos_f32) unless RB_FAST_TRIG=0.
+bool fast_trig() {
+    static const bool fast = env_flag("RB_FAST_TRIG", true);
+    return fast;
+}
+
+struct DeviceConsts {
+    float *f32 = nullptr;
+    double *f64 = nullptr;
+};
+
+}  // namespace
+
+struct Multibody {
+    rbamd::Model model;
+    std::vector<float> pk32;
+    std::vector<double> pk64;
+    mutable std::mutex mu;
+    mutable std::map<int, DeviceConsts> dev;
+};
+
+namespace {
+
+Multibody *make(rbamd::Model &&m) {
+    if (!m.all_axes_z()) {
+        set_err(RB_ERR_UNSUPPORTED,
+                "non-z joint axis: the reference injects joint motion about local z "
+                "(multibody.rs:130-138,144); only z-axis chains are supported");
+        return nullptr;
+    }
+    if (!rbamd::dof_supported(m.n)) {
+        set_err(RB_ERR_DOF, "no kernel compiled for " + std::to_string(m.n) + " DOF");
+        return nullptr;
+    }
+    Multibody *mb = new Multibody();
+    mb->pk32 = m.pack_f32();
+    mb->pk64 = m.pack_f64();
+    mb->model = std::move(m);
+    return mb;
+}
+
+// Device copy of the packed model constants on the current device (uploaded once).
+template <typename T>
+int device_consts(const Multibody *mb, const T **out) {
+    int d = 0;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess) return hip_err(e, "hipGetDevice");
+    std::lock_guard<std::mutex> lk(mb->mu);
+    DeviceConsts &dc = mb->dev[d];
+    if constexpr (sizeof(T) == 4) {
+        if (!dc.f32) {
+            void *p = nullptr;
+            size_t bytes = mb->pk32.size() * sizeof(float);
+            if ((e = hipMalloc(&p, bytes)) != hipSuccess) return hip_err(e, "hipMalloc(model)");
+            if ((e = hipMemcpy(p, mb->pk32.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) {
+                (void)hipFree(p);
+                return hip_err(e, "hipMemcpy(model)");
+            }
+            dc.f32 = static_cast<float *>(p);
+        }
+        *out = reinterpret_cast<const T *>(dc.f32);
+    } else {
+        if (!dc.f64) {
+            void *p = nullptr;
+            size_t bytes = mb->pk64.size() * sizeof(double);
+            if ((e = hipMalloc(&p, bytes)) != hipSuccess) return hip_err(e, "hipMalloc(model)");
+            if ((e = hipMemcpy(p, mb->pk64.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) {
+                (void)hipFree(p);
+                return hip_err(e, "hipMemcpy(model)");
+            }
+            dc.f64 = static_cast<double *>(p);
+        }
+        *out = reinterpret_cast<const T *>(dc.f64);
+    }
+    return RB_OK;
+}
+
+constexpr int64_t kChunk = int64_t(1) << 28;  // per-launch batch cap: b * sizeof(T) < 2^32
+
+int check_batch(const Multibody *mb, int64_t batch, int64_t ld) {
+    if (!mb) return set_err(RB_ERR_NULL, "NULL Multibody handle");
+    if (batch < 0) return set_err(RB_ERR_ARG, "negative batch");
+    if (ld < batch) return set_err(RB_ERR_ARG, "leading dimension ld < batch");
+    return RB_OK;
+}
+
+// Thread-local staging for the single-configuration ABI: one stream, one device
+// buffer and one pinned host buffer per thread and device (never freed: HIP teardown
+// order at process exit is not ours to control).
+struct Staging {
+    hipStream_t stream = nullptr;
+    double *dbuf = nullptr;
+    size_t dcap = 0;
+    double *hbuf = nullptr;
+    size_t hcap = 0;
+};
+thread_local std::map<int, Staging> t_staging;
+
+int staging(size_t doubles, Staging **out) {
+    int d = 0;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess) return hip_err(e, "hipGetDevice");
+    Staging &s = t_staging[d];
+    if (!s.stream) {
+        if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
+            return hip_err(e, "hipStreamCreate");
+    }
+    if (s.dcap < doubles) {
+        if (s.dbuf) (void)hipFree(s.dbuf);
+        s.dbuf = nullptr;
+        s.dcap = 0;
+        if ((e = hipMalloc(&s.dbuf, doubles * sizeof(double))) != hipSuccess) return hip_err(e, "hipMalloc");
+        s.dcap = doubles;
+    }
+    if (s.hcap < doubles) {
+        if (s.hbuf) (void)hipHostFree(s.hbuf);
+        s.hbuf = nullptr;
+        s.hcap = 0;
+        if ((e = hipHostMalloc(&s.hbuf, doubles * sizeof(double), hipHostMallocDefault)) != hipSuccess)
+            return hip_err(e, "hipHostMalloc");
+        s.hcap = doubles;
+    }
+    *out = &s;
+    return RB_OK;
+}
+
+// Runs one single-configuration query on the GPU: `nin` input vectors of n doubles,
+// `nout` output doubles; `launch(dev_in, dev_out, stream)` enqueues the kernel.
+template <typename F>
+double *single_query(const Multibody *mb, const double *const *inputs, int nin, size_t nout, F launch) {
+    if (!mb) { set_err(RB_ERR_NULL, "NULL Multibody handle"); return nullptr; }
+    const int n = mb->model.n;
+    for (int k = 0; k < nin; ++k)
+        if (!inputs[k]) { set_err(RB_ERR_NULL, "NULL input vector"); return nullptr; }
+    Staging *s = nullptr;
+    const size_t total = (size_t)nin * n + nout;
+    if (staging(total, &s) != RB_OK) return nullptr;
+    for (int k = 0; k < nin; ++k) std::memcpy(s->hbuf + (size_t)k * n, inputs[k], n * sizeof(double));
+    hipError_t e = hipMemcpyAsync(s->dbuf, s->hbuf, (size_t)nin * n * sizeof(double), hipMemcpyHostToDevice, s->stream);
+    if (e != hipSuccess) { hip_err(e, "hipMemcpyAsync H2D"); return nullptr; }
+    int rc = launch(s->dbuf, s->dbuf + (size_t)nin * n, s->stream);
+    if (rc != RB_OK) return nullptr;
+    e = hipMemcpyAsync(s->hbuf + (size_t)nin * n, s->dbuf + (size_t)nin * n, nout * sizeof(double), hipMemcpyDeviceToHost, s->stream);
+    if (e != hipSuccess) { hip_err(e, "hipMemcpyAsync D2H"); return nullptr; }
+    if ((e = hipStreamSynchronize(s->stream)) != hipSuccess) { hip_err(e, "hipStreamSynchronize"); return nullptr; }
+    double *res = static_cast<double *>(std::malloc(nout * sizeof(double)));
+    if (!res) { set_err(RB_ERR_ARG, "out of host memory"); return nullptr; }
+    std::memcpy(res, s->hbuf + (size_t)nin * n, nout * sizeof(double));
+    return res;
+}
+
+template <typename T, typename L>
+int chunked(int64_t batch, L &&one) {
+    for (int64_t b0 = 0; b0 < batch; b0 += kChunk) {
+        const int64_t nb = batch - b0 < kChunk ? batch - b0 : kChunk;
+        int rc = one(b0, (uint32_t)nb);
+        if (rc != RB_OK) return rc;
+    }
+    return RB_OK;
+}
+
+template <typename T>
+int rnea_batch(const Multibody *mb, const T *q, const T *qd, const T *qdd, T *tau, int64_t batch,
+               int64_t ld, void *stream) {
+    int rc = check_batch(mb, batch, ld);
+    if (rc) return rc;
+    if (batch == 0) return RB_OK;
+    if (!q || !qd || !qdd || !tau) return set_err(RB_ERR_NULL, "NULL array");
+    const T *mdl = nullptr;
+    if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
+        hipError_t e = rbamd::launch_rnea<T>(mb->model.n, mdl, q + b0, qd + b0, qdd + b0, tau + b0, nb, ld,
+                                             (hipStream_t)stream, fast_trig());
+        return e == hipSuccess ? RB_OK : hip_err(e, "rnea launch");
+    });
+}
+
+template <typename T>
+int fd_batch(const Multibody *mb, const T *q, const T *qd, const T *tau, T *qdd, int64_t batch,
+             int64_t ld, void *stream) {
+    int rc = check_batch(mb, batch, ld);
+    if (rc) return rc;
+    if (batch == 0) return RB_OK;
+    if (!q || !qd || !tau || !qdd) return set_err(RB_ERR_NULL, "NULL array");
+    const T *mdl = nullptr;
+    if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
+        hipError_t e = rbamd::launch_aba<T>(mb->model.n, mdl, q + b0, qd + b0, tau + b0, qdd + b0, nb, ld,
+                                            (hipStream_t)stream, fast_trig());
+        return e == hipSuccess ? RB_OK : hip_err(e, "aba launch");
+    });
+}
+
+template <typename T>
+int crba_batch(const Multibody *mb, const T *q, T *H, int64_t batch, int64_t ld, void *stream) {
+    int rc = check_batch(mb, batch, ld);
+    if (rc) return rc;
+    if (batch == 0) return RB_OK;
+    if (!q || !H) return set_err(RB_ERR_NULL, "NULL array");
+    const T *mdl = nullptr;
+    if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
+        hipError_t e = rbamd::launch_crba<T>(mb->model.n, mdl, q + b0, H + b0, nb, ld, (hipStream_t)stream);
+        return e == hipSuccess ? RB_OK : hip_err(e, "crba launch");
+    });
+}
+
+Multibody *new_from_text(const std::string &xml) {
+    try {
+        return make(rbamd::Model::from_urdf_text(xml));
+    } catch (const std::exception &ex) {
+        set_err(RB_ERR_URDF, ex.what());
+        return nullptr;
+    }
+}
+
+}  // namespace
+
+namespace {
+template <typename Launch>
+int host_batch(const Multibody *mb, const double *const *in, int nin, double *out, int64_t batch, Launch launch) {
+    int rc = check_batch(mb, batch, batch);
+    if (rc) return rc;
+    if (batch == 0) return RB_OK;
+    for (int k = 0; k < nin; ++k)
+        if (!in[k]) return set_err(RB_ERR_NULL, "NULL array");
+    if (!out) return set_err(RB_ERR_NULL, "NULL array");
+    const size_t per = (size_t)mb->model.n * (size_t)batch;
+    double *d = nullptr;
+    hipStream_t s = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_err(e, "hipStreamCreate");
+    e = hipMallocAsync((void **)&d, per * (nin + 1) * sizeof(double), s);
+    if (e != hipSuccess) { (void)hipStreamDestroy(s); return hip_err(e, "hipMallocAsync"); }
+    for (int k = 0; k < nin && e == hipSuccess; ++k)
+        e = hipMemcpyAsync(d + k * per, in[k], per * sizeof(double), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) rc = launch(d, d + nin * per, s);
+    else rc = hip_err(e, "hipMemcpyAsync H2D");
+    if (rc == RB_OK) {
+        e = hipMemcpyAsync(out, d + nin * per, per * sizeof(double), hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) rc = hip_err(e, "hipMemcpyAsync D2H");
+    }
+    (void)hipFreeAsync(d, s);
+    e = hipStreamSynchronize(s);
+    if (rc == RB_OK && e != hipSuccess) rc = hip_err(e, "hipStreamSynchronize");
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+}  // namespace
+
+namespace {
+template <typename T>
+int fill_uniform(T *x, int rows, int64_t batch, int64_t ld, const double *lo, const double *hi, uint64_t seed,
+                 void *stream) {
+    if (!x || !lo || !hi) return set_err(RB_ERR_NULL, "NULL argument");
+    if (rows < 1 || batch < 0 || ld < batch || batch >= (int64_t(1) << 40))
+        return set_err(RB_ERR_ARG, "bad fill shape");
+    if (batch == 0) return RB_OK;
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<double> lohi(2 * (size_t)rows);
+    for (int j = 0; j < rows; ++j) {
+        lohi[2 * j] = lo[j];
+        lohi[2 * j + 1] = hi[j];
+    }
+    double *d = nullptr;
+    hipError_t e = hipMallocAsync((void **)&d, lohi.size() * sizeof(double), s);
+    if (e != hipSuccess) return hip_err(e, "hipMallocAsync");
+    e = hipMemcpyAsync(d, lohi.data(), lohi.size() * sizeof(double), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_err(e, "hipMemcpyAsync");
+    int rc = RB_OK;
+    for (int64_t b0 = 0; b0 < batch && rc == RB_OK; b0 += kChunk) {
+        const int64_t nb = batch - b0 < kChunk ? batch - b0 : kChunk;
+        // the generator indexes by the absolute configuration index b0 + b
+        e = rbamd::launch_fill_uniform<T>(x + b0, rows, (uint32_t)nb, ld, d, seed, s);
+        if (e != hipSuccess) rc = hip_err(e, "fill launch");
+        if (b0 + kChunk < batch) { rc = set_err(RB_ERR_ARG, "fill batch above 2^30 not supported"); }
+    }
+    (void)hipFreeAsync(d, s);
+    // the host-side lohi vector dies here; make sure the copy has consumed it
+    e = hipStreamSynchronize(s);
+    if (rc == RB_OK && e != hipSuccess) rc = hip_err(e, "hipStreamSynchronize");
+    return rc;
+}
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------- reference ABI (6)
+Multibody *multibody_new(void) {
+    if (const char *path = std::getenv("RIGIDBODY_URDF")) {
+        if (*path) return multibody_new_from_urdf(path);
+    }
+    return new_from_text(std::string(kFr3Urdf));
+}
+
+void multibody_free(Multibody *mb) {
+    if (!mb) return;
+    int cur = 0;
+    bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    for (auto &kv : mb->dev) {
+        if (hipSetDevice(kv.first) != hipSuccess) continue;
+        if (kv.second.f32) (void)hipFree(kv.second.f32);
+        if (kv.second.f64) (void)hipFree(kv.second.f64);
+    }
+    if (have_cur) (void)hipSetDevice(cur);
+    delete mb;
+}
+
+double *multibody_rnea(const Multibody *mb, const double *q, const double *dq, const double *ddq) {
+    const double *in[3] = {q, dq, ddq};
+    const size_t n = mb ? (size_t)mb->model.n : 0;
+    return single_query(mb, in, 3, n, [&](double *din, double *dout, hipStream_t s) {
+        const double *mdl = nullptr;
+        int rc = device_consts<double>(mb, &mdl);
+        if (rc) return rc;
+        hipError_t e = rbamd::launch_rnea<double>((int)n, mdl, din, din + n, din + 2 * n, dout, 1, 1, s, false);
+        return e == hipSuccess ? RB_OK : hip_err(e, "rnea launch");
+    });
+}
+
+double *multibody_crba(const Multibody *mb, const double *q) {
+    const double *in[1] = {q};
+    const size_t n = mb ? (size_t)mb->model.n : 0;
+    return single_query(mb, in, 1, n * n, [&](double *din, double *dout, hipStream_t s) {
+        const double *mdl = nullptr;
+        int rc = device_consts<double>(mb, &mdl);
+        if (rc) return rc;
+        hipError_t e = rbamd::launch_crba<double>((int)n, mdl, din, dout, 1, 1, s);
+        return e == hipSuccess ? RB_OK : hip_err(e, "crba launch");
+    });
+}
+
+double *multibody_fwd_kin(const Multibody *mb, const double *q) {
+    const double *in[1] = {q};
+    const size_t n = mb ? (size_t)mb->model.n : 0;
+    return single_query(mb, in, 1, 3, [&](double *din, double *dout, hipStream_t s) {
+        const double *mdl = nullptr;
+        int rc = device_consts<double>(mb, &mdl);
+        if (rc) return rc;
+        hipError_t e = rbamd::launch_fwd_kin<double>((int)n, mdl, din, dout, 1, 1, s);
+        return e == hipSuccess ? RB_OK : hip_err(e, "fwd_kin launch");
+    });
+}
+
+double *multibody_jac(const Multibody *mb, const double *q) {
+    const double *in[1] = {q};
+    const size_t n = mb ? (size_t)mb->model.n : 0;
+    return single_query(mb, in, 1, 6 * n, [&](double *din, double *dout, hipStream_t s) {
+        const double *mdl = nullptr;
+        int rc = device_consts<double>(mb, &mdl);
+        if (rc) return rc;
+        hipError_t e = rbamd::launch_jac<double>((int)n, mdl, din, dout, 1, 1, s);
+        return e == hipSuccess ? RB_OK : hip_err(e, "jac launch");
+    });
+}
+
+// ---------------------------------------------------------------- model handling
+Multibody *multibody_new_from_urdf(const char *path) {
+    if (!path) { set_err(RB_ERR_NULL, "NULL path"); return nullptr; }
+    std::ifstream f(path, std::ios::binary);
+    if (!f) { set_err(RB_ERR_URDF, std::string("cannot open URDF: ") + path); return nullptr; }
+    std::stringstream ss;
+    ss << f.rdbuf();
+    return new_from_text(ss.str());
+}
+
+Multibody *multibody_new_from_urdf_string(const char *xml, size_t len) {
+    if (!xml) { set_err(RB_ERR_NULL, "NULL URDF string"); return nullptr; }
+    return new_from_text(std::string(xml, len));
+}
+
+int64_t multibody_blob_size(const Multibody *mb) {
+    if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
+    return rbamd::kBlobHeader + (int64_t)mb->model.n * rbamd::kBlobPerLink;
+}
+
+int multibody_export_blob(const Multibody *mb, double *out, int64_t len) {
+    if (!mb || !out) return set_err(RB_ERR_NULL, "NULL argument");
+    std::vector<double> b = mb->model.blob();
+    if (len < (int64_t)b.size()) return set_err(RB_ERR_ARG, "blob buffer too small");
+    std::memcpy(out, b.data(), b.size() * sizeof(double));
+    return RB_OK;
+}
+
+Multibody *multibody_new_from_blob(const double *blob, int64_t len) {
+    try {
+        return make(rbamd::Model::from_blob(blob, len));
+    } catch (const std::exception &ex) {
+        set_err(RB_ERR_ARG, ex.what());
+        return nullptr;
+    }
+}
+
+int multibody_dof(const Multibody *mb) { return mb ? mb->model.n : -set_err(RB_ERR_NULL, "NULL Multibody handle"); }
+
+double multibody_total_mass(const Multibody *mb) {
+    if (!mb) { set_err(RB_ERR_NULL, "NULL Multibody handle"); return std::nan(""); }
+    return mb->model.total_mass();
+}
+
+int multibody_limits(const Multibody *mb, double *lower, double *upper, double *velocity, double *effort) {
+    if (!mb) return set_err(RB_ERR_NULL, "NULL Multibody handle");
+    for (int i = 0; i < mb->model.n; ++i) {
+        const rbamd::LinkModel &L = mb->model.links[i];
+        if (lower) lower[i] = L.lower;
+        if (upper) upper[i] = L.upper;
+        if (velocity) velocity[i] = L.velocity;
+        if (effort) effort[i] = L.effort;
+    }
+    return RB_OK;
+}
+
+int multibody_supported_dofs(int *out, int cap) { return rbamd::supported_dofs(out, cap); }
+
+int multibody_upload(const Multibody *mb) {
+    if (!mb) return set_err(RB_ERR_NULL, "NULL Multibody handle");
+    const float *a = nullptr;
+    const double *b = nullptr;
+    int rc = device_consts<float>(mb, &a);
+    if (rc) return rc;
+    return device_consts<double>(mb, &b);
+}
+
+void multibody_result_free(double *p) { std::free(p); }
+const char *rb_last_error(void) { return g_last_error.c_str(); }
+const char *rb_version(void) { return RB_VERSION; }
+
+// ------------------------------------------------------------- batched (device)
+int multibody_rnea_batch_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                             float *tau, int64_t batch, int64_t ld, void *stream) {
+    return rnea_batch<float>(mb, q, qd, qdd, tau, batch, ld, stream);
+}
+int multibody_rnea_batch_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                             double *tau, int64_t batch, int64_t ld, void *stream) {
+    return rnea_batch<double>(mb, q, qd, qdd, tau, batch, ld, stream);
+}
+int multibody_fd_batch_f32(const Multibody *mb, const float *q, const float *qd, const float *tau,
+                           float *qdd, int64_t batch, int64_t ld, void *stream) {
+    return fd_batch<float>(mb, q, qd, tau, qdd, batch, ld, stream);
+}
+int multibody_fd_batch_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
+                           double *qdd, int64_t batch, int64_t ld, void *stream) {
+    return fd_batch<double>(mb, q, qd, tau, qdd, batch, ld, stream);
+}
+int multibody_crba_batch_f32(const Multibody *mb, const float *q, float *H, int64_t batch, int64_t ld,
+                             void *stream) {
+    return crba_batch<float>(mb, q, H, batch, ld, stream);
+}
+int multibody_crba_batch_f64(const Multibody *mb, const double *q, double *H, int64_t batch, int64_t ld,
+                             void *stream) {
+    return crba_batch<double>(mb, q, H, batch, ld, stream);
+}
+
+int multibody_fwd_kin_batch_f64(const Multibody *mb, const double *q, double *pos, int64_t batch,
+                                int64_t ld, void *stream) {
+    int rc = check_batch(mb, batch, ld);
+    if (rc) return rc;
+    if (batch == 0) return RB_OK;
+    if (!q || !pos) return set_err(RB_ERR_NULL, "NULL array");
+    const double *mdl = nullptr;
+    if ((rc = device_consts<double>(mb, &mdl))) return rc;
+    return chunked<double>(batch, [&](int64_t b0, uint32_t nb) {
+        hipError_t e = rbamd::launch_fwd_kin<double>(mb->model.n, mdl, q + b0, pos + b0, nb, ld, (hipStream_t)stream);
+        return e == hipSuccess ? RB_OK : hip_err(e, "fwd_kin launch");
+    });
+}
+
+int multibody_jac_batch_f64(const Multibody *mb, const double *q, double *J, int64_t batch, int64_t ld,
+                            void *stream) {
+    int rc = check_batch(mb, batch, ld);
+    if (rc) return rc;
+    if (batch == 0) return RB_OK;
+    if (!q || !J) return set_err(RB_ERR_NULL, "NULL array");
+    const double *mdl = nullptr;
+    if ((rc = device_consts<double>(mb, &mdl))) return rc;
+    return chunked<double>(batch, [&](int64_t b0, uint32_t nb) {
+        hipError_t e = rbamd::launch_jac<double>(mb->model.n, mdl, q + b0, J + b0, nb, ld, (hipStream_t)stream);
+        return e == hipSuccess ? RB_OK : hip_err(e, "jac launch");
+    });
+}
+
+// ------------------------------------------------------------- batched (host)
+
+int multibody_rnea_batch_host_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                  double *tau, int64_t batch) {
+    const double *in[3] = {q, qd, qdd};
+    return host_batch(mb, in, 3, tau, batch, [&](double *d, double *o, hipStream_t s) {
+        const size_t per = (size_t)mb->model.n * (size_t)batch;
+        return rnea_batch<double>(mb, d, d + per, d + 2 * per, o, batch, batch, s);
+    });
+}
+
+int multibody_fd_batch_host_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
+                                double *qdd, int64_t batch) {
+    const double *in[3] = {q, qd, tau};
+    return host_batch(mb, in, 3, qdd, batch, [&](double *d, double *o, hipStream_t s) {
+        const size_t per = (size_t)mb->model.n * (size_t)batch;
+        return fd_batch<double>(mb, d, d + per, d + 2 * per, o, batch, batch, s);
+    });
+}
+
+// ------------------------------------------------------------- synthetic inputs
+
+int rb_fill_uniform_f32(float *x, int n_rows, int64_t batch, int64_t ld, const double *lo, const double *hi,
+                        uint64_t seed, void *stream) {
+    return fill_uniform<float>(x, n_rows, batch, ld, lo, hi, seed, stream);
+}
+int rb_fill_uniform_f64(double *x, int n_rows, int64_t batch, int64_t ld, const double *lo, const double *hi,
+                        uint64_t seed, void *stream) {
+    return fill_uniform<double>(x, n_rows, batch, ld, lo, hi, seed, stream);
+}
+
+}  // extern "C"

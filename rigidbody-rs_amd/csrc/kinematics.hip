@@ -1,0 +1,172 @@
+// kinematics.hip -- batched fwd_kin / jac (multibody.rs:87-108) and synthetic input fill.
+// Shared design notes: kernels.hpp.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dofs.hpp"
+#include "kernels.hpp"
+#include "spatial.hip.hpp"
+
+namespace rbamd {
+namespace dev {
+
+// ------------------------------------------------------------------- fwd_kin / jac
+template <typename T, int N, bool FAST>
+__global__ __launch_bounds__(kBlock) void fwd_kin_kernel(const T *__restrict__ gmdl,
+                                                         const T *__restrict__ q,
+                                                         T *__restrict__ pos, uint32_t B,
+                                                         int64_t ld) {
+    __shared__ T mdl[N * kLinkStride];
+    stage_model<T, N, kBlock>(gmdl, mdl);
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= B) return;
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    // T_0 T_1 ... T_{n-1} accumulated from the base: p += R p_i, R = R E_i
+    M3<T> R{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
+    V3<T> p = v3(T(0), T(0), T(0));
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const Link<T> L = load_link(mdl, j);
+        T s, c;
+        sin_cos<FAST>(ld_row(q, j * ld, off), s, c);
+        const M3<T> E = joint_rotation(L.Rp, c, s);
+        p = mul_add(p, R, L.p);
+        M3<T> Rn;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc)
+                Rn.m[3 * r + cc] = fmadd(R.m[3 * r + 0], E.m[cc], fmadd(R.m[3 * r + 1], E.m[3 + cc], R.m[3 * r + 2] * E.m[6 + cc]));
+        R = Rn;
+    }
+    st_row(pos, 0 * ld, off, p.x);
+    st_row(pos, 1 * ld, off, p.y);
+    st_row(pos, 2 * ld, off, p.z);
+}
+
+template <typename T, int N, bool FAST>
+__global__ __launch_bounds__(kBlock) void jac_kernel(const T *__restrict__ gmdl,
+                                                     const T *__restrict__ q,
+                                                     T *__restrict__ J, uint32_t B,
+                                                     int64_t ld) {
+    __shared__ T mdl[N * kLinkStride];
+    stage_model<T, N, kBlock>(gmdl, mdl);
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= B) return;
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    // acc = pose of the last frame in frame i, built leaf -> root (multibody.rs:97-106):
+    // column i = motion transform of S_i = (0,0,1 | 0) by acc:
+    //   rot = R^T z,  lin = R^T (0 - p x z) = -R^T (p.y, -p.x, 0)
+    M3<T> R{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
+    V3<T> p = v3(T(0), T(0), T(0));
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        const V3<T> rot = v3(R.m[6], R.m[7], R.m[8]);
+        const V3<T> lin = mul_t(R, v3(-p.y, p.x, T(0)));
+        st_row(J, (6 * i + 0) * ld, off, lin.x);
+        st_row(J, (6 * i + 1) * ld, off, lin.y);
+        st_row(J, (6 * i + 2) * ld, off, lin.z);
+        st_row(J, (6 * i + 3) * ld, off, rot.x);
+        st_row(J, (6 * i + 4) * ld, off, rot.y);
+        st_row(J, (6 * i + 5) * ld, off, rot.z);
+        const Link<T> L = load_link(mdl, i);
+        T s, c;
+        sin_cos<FAST>(ld_row(q, i * ld, off), s, c);
+        const M3<T> E = joint_rotation(L.Rp, c, s);
+        // acc <- T_i * acc = (E R, p_i + E p)
+        p = mul_add(L.p, E, p);
+        M3<T> Rn;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc)
+                Rn.m[3 * r + cc] = fmadd(E.m[3 * r + 0], R.m[cc], fmadd(E.m[3 * r + 1], R.m[3 + cc], E.m[3 * r + 2] * R.m[6 + cc]));
+        R = Rn;
+    }
+}
+
+// ---------------------------------------------------------------- synthetic inputs
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void fill_uniform_kernel(T *__restrict__ x, int rows,
+                                                              uint32_t B, int64_t ld,
+                                                              const double *__restrict__ lohi,
+                                                              uint64_t seed) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= B) return;
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    for (int j = 0; j < rows; ++j) {
+        const uint64_t idx = ((uint64_t)j << 40) | (uint64_t)b;
+        const uint64_t u = splitmix64(seed * 0x9E3779B97F4A7C15ull + idx + 1ull);
+        double r;
+        if constexpr (sizeof(T) == 8) {
+            r = (double)(u >> 11) * 0x1.0p-53;
+        } else {
+            r = (double)(u >> 40) * 0x1.0p-24;
+        }
+        const double lo = lohi[2 * j], hi = lohi[2 * j + 1];
+        // no FMA contraction: the host reproduction (chains.host_uniform) rounds the
+        // product and the sum separately
+        st_row(x, j * ld, off, (T)__dadd_rn(lo, __dmul_rn(hi - lo, r)));
+    }
+}
+
+}  // namespace dev
+
+template <typename T>
+hipError_t launch_fwd_kin(int n, const T *mdl, const T *q, T *pos, uint32_t B, int64_t ld,
+                          hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    const dim3 grid(dev::grid_for(B)), block(dev::kBlock);
+    switch (n) {
+#define RB_CASE(N)                                                                              \
+    case N:                                                                                     \
+        hipLaunchKernelGGL((dev::fwd_kin_kernel<T, N, false>), grid, block, 0, s, mdl, q, pos, B, ld); \
+        break;
+        RB_FOR_EACH_DOF(RB_CASE)
+#undef RB_CASE
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_jac(int n, const T *mdl, const T *q, T *J, uint32_t B, int64_t ld,
+                      hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    const dim3 grid(dev::grid_for(B)), block(dev::kBlock);
+    switch (n) {
+#define RB_CASE(N)                                                                              \
+    case N:                                                                                     \
+        hipLaunchKernelGGL((dev::jac_kernel<T, N, false>), grid, block, 0, s, mdl, q, J, B, ld); \
+        break;
+        RB_FOR_EACH_DOF(RB_CASE)
+#undef RB_CASE
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_fill_uniform(T *x, int rows, uint32_t B, int64_t ld, const double *lohi_dev,
+                               uint64_t seed, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    hipLaunchKernelGGL((dev::fill_uniform_kernel<T>), dim3(dev::grid_for(B)), dim3(dev::kBlock), 0, s,
+                       x, rows, B, ld, lohi_dev, seed);
+    return hipGetLastError();
+}
+
+template hipError_t launch_fwd_kin<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t);
+template hipError_t launch_jac<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t);
+template hipError_t launch_fill_uniform<float>(float *, int, uint32_t, int64_t, const double *, uint64_t, hipStream_t);
+template hipError_t launch_fill_uniform<double>(double *, int, uint32_t, int64_t, const double *, uint64_t, hipStream_t);
+
+}  // namespace rbamd

@@ -1,0 +1,22 @@
+// layout.hpp -- packed per-link model constants shared by host (model.cpp) and device.
+#pragma once
+
+namespace rbamd {
+
+// Scalars per link in the device constant block.
+constexpr int kLinkStride = 24;
+// Offsets inside one link's block.
+enum : int {
+    kE0 = 0,    // parent rotation matrix R_p, row-major (9)
+    kP = 9,     // parent translation p (3)
+    kM = 12,    // mass
+    kH = 13,    // first mass moment h = m * com (3)
+    kIo = 16,   // inertia about the link origin, symmetric: xx xy xz yy yz zz (6)
+    kPad = 22,  // 2 unused
+};
+
+// Base acceleration: the reference's fictitious-gravity trick, +9.81 along base z
+// (multibody.rs:117-120).
+constexpr double kGravity = 9.81;
+
+}  // namespace rbamd

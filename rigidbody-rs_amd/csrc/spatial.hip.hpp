@@ -1,0 +1,241 @@
+// spatial.hip.hpp -- per-lane spatial algebra for the batched kernels (device only).
+//
+// One GPU lane owns one configuration; everything below is straight-line register
+// arithmetic on 3-vectors, written with explicit FMAs so the instruction count is
+// what the roofline in DESIGN.md assumes.  Conventions follow the reference:
+//   spatial vectors are (rot, lin) pairs, Featherstone ordering (spatial.rs:137-149);
+//   link pose T_i = (E_i, p_i), E_i = R_p,i * Rz(q_i)   (joint.rs:36-38, 48-50)
+//   motion parent->child:  w' = E^T w,  v' = E^T (v - p x w)      (spatial.rs:110-116)
+//   force  child->parent:  f' = E f,    n' = E n + p x (E f)      (spatial.rs:242-248
+//                                                                  with Isometry::inverse)
+//   rigid-body inertia (m, h = m c, I_o):  I*(w,v) = (I_o w + h x v,  m v - h x w)
+//                                                                  (inertia.rs:107-117)
+//   v x* f = (w x n + v x f,  w x f)                               (spatial.rs:129-134)
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "layout.hpp"
+
+namespace rbamd {
+namespace dev {
+
+__device__ __forceinline__ float fmadd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fmadd(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+template <typename T>
+struct V3 {
+    T x, y, z;
+};
+
+template <typename T>
+__device__ __forceinline__ V3<T> v3(T x, T y, T z) { return V3<T>{x, y, z}; }
+
+// a x b
+template <typename T>
+__device__ __forceinline__ V3<T> cross(const V3<T> &a, const V3<T> &b) {
+    return v3(fmadd(a.y, b.z, -a.z * b.y), fmadd(a.z, b.x, -a.x * b.z), fmadd(a.x, b.y, -a.y * b.x));
+}
+
+// acc + a x b
+template <typename T>
+__device__ __forceinline__ V3<T> cross_add(const V3<T> &acc, const V3<T> &a, const V3<T> &b) {
+    return v3(fmadd(a.y, b.z, fmadd(-a.z, b.y, acc.x)), fmadd(a.z, b.x, fmadd(-a.x, b.z, acc.y)),
+              fmadd(a.x, b.y, fmadd(-a.y, b.x, acc.z)));
+}
+
+// acc - a x b
+template <typename T>
+__device__ __forceinline__ V3<T> cross_sub(const V3<T> &acc, const V3<T> &a, const V3<T> &b) {
+    return v3(fmadd(-a.y, b.z, fmadd(a.z, b.y, acc.x)), fmadd(-a.z, b.x, fmadd(a.x, b.z, acc.y)),
+              fmadd(-a.x, b.y, fmadd(a.y, b.x, acc.z)));
+}
+
+// Row-major 3x3.
+template <typename T>
+struct M3 {
+    T m[9];
+};
+
+// M x
+template <typename T>
+__device__ __forceinline__ V3<T> mul(const M3<T> &M, const V3<T> &x) {
+    return v3(fmadd(M.m[0], x.x, fmadd(M.m[1], x.y, M.m[2] * x.z)),
+              fmadd(M.m[3], x.x, fmadd(M.m[4], x.y, M.m[5] * x.z)),
+              fmadd(M.m[6], x.x, fmadd(M.m[7], x.y, M.m[8] * x.z)));
+}
+
+// acc + M x
+template <typename T>
+__device__ __forceinline__ V3<T> mul_add(const V3<T> &acc, const M3<T> &M, const V3<T> &x) {
+    return v3(fmadd(M.m[0], x.x, fmadd(M.m[1], x.y, fmadd(M.m[2], x.z, acc.x))),
+              fmadd(M.m[3], x.x, fmadd(M.m[4], x.y, fmadd(M.m[5], x.z, acc.y))),
+              fmadd(M.m[6], x.x, fmadd(M.m[7], x.y, fmadd(M.m[8], x.z, acc.z))));
+}
+
+// M^T x
+template <typename T>
+__device__ __forceinline__ V3<T> mul_t(const M3<T> &M, const V3<T> &x) {
+    return v3(fmadd(M.m[0], x.x, fmadd(M.m[3], x.y, M.m[6] * x.z)),
+              fmadd(M.m[1], x.x, fmadd(M.m[4], x.y, M.m[7] * x.z)),
+              fmadd(M.m[2], x.x, fmadd(M.m[5], x.y, M.m[8] * x.z)));
+}
+
+// Symmetric 3x3: xx xy xz yy yz zz
+template <typename T>
+struct S3 {
+    T xx, xy, xz, yy, yz, zz;
+};
+
+template <typename T>
+__device__ __forceinline__ V3<T> mul(const S3<T> &S, const V3<T> &x) {
+    return v3(fmadd(S.xx, x.x, fmadd(S.xy, x.y, S.xz * x.z)),
+              fmadd(S.xy, x.x, fmadd(S.yy, x.y, S.yz * x.z)),
+              fmadd(S.xz, x.x, fmadd(S.yz, x.y, S.zz * x.z)));
+}
+
+template <typename T>
+__device__ __forceinline__ V3<T> mul_add(const V3<T> &acc, const S3<T> &S, const V3<T> &x) {
+    return v3(fmadd(S.xx, x.x, fmadd(S.xy, x.y, fmadd(S.xz, x.z, acc.x))),
+              fmadd(S.xy, x.x, fmadd(S.yy, x.y, fmadd(S.yz, x.z, acc.y))),
+              fmadd(S.xz, x.x, fmadd(S.yz, x.y, fmadd(S.zz, x.z, acc.z))));
+}
+
+// Per-link model constants.  Each workgroup first copies the packed block (layout.hpp,
+// n * 24 scalars, <= 5.8 KB) from HBM/L2 into LDS (stage_model); every later read is a
+// wave-uniform LDS broadcast, issued where the link is processed.  (Reading the block
+// with scalar loads instead makes the compiler hoist all n*22 constants into SGPRs and
+// spill them: 58 spills at fp32 / 224 at fp64 for the 7-DOF RNEA.)
+template <typename T>
+struct Link {
+    M3<T> Rp;
+    V3<T> p;
+    T m;
+    V3<T> h;
+    S3<T> Io;
+};
+
+template <typename T, int N, int BLOCK>
+__device__ __forceinline__ void stage_model(const T *__restrict__ mdl, T *smem) {
+#pragma unroll
+    for (int k = threadIdx.x; k < N * kLinkStride; k += BLOCK) smem[k] = mdl[k];
+    __syncthreads();
+}
+
+template <typename T>
+__device__ __forceinline__ Link<T> load_link(const T *__restrict__ mdl, int i) {
+    const T *c = mdl + i * kLinkStride;
+    Link<T> L;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) L.Rp.m[k] = c[kE0 + k];
+    L.p = v3(c[kP + 0], c[kP + 1], c[kP + 2]);
+    L.m = c[kM];
+    L.h = v3(c[kH + 0], c[kH + 1], c[kH + 2]);
+    L.Io = S3<T>{c[kIo + 0], c[kIo + 1], c[kIo + 2], c[kIo + 3], c[kIo + 4], c[kIo + 5]};
+    return L;
+}
+
+// E = R_p * Rz(q): columns 0/1 mix with (cos, sin), column 2 is R_p's.
+template <typename T>
+__device__ __forceinline__ M3<T> joint_rotation(const M3<T> &Rp, T c, T s) {
+    M3<T> E;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const T a = Rp.m[3 * r + 0], b = Rp.m[3 * r + 1];
+        E.m[3 * r + 0] = fmadd(a, c, b * s);
+        E.m[3 * r + 1] = fmadd(b, c, -a * s);
+        E.m[3 * r + 2] = Rp.m[3 * r + 2];
+    }
+    return E;
+}
+
+// Rigid-body inertia times a motion vector (inertia.rs:107-117); returns (rot, lin).
+template <typename T>
+__device__ __forceinline__ void inertia_mul(const Link<T> &L, const V3<T> &w, const V3<T> &v,
+                                            V3<T> &n, V3<T> &f) {
+    n = cross_add(mul(L.Io, w), L.h, v);                     // I_o w + h x v
+    f = cross_sub(v3(L.m * v.x, L.m * v.y, L.m * v.z), L.h, w);  // m v - h x w
+}
+
+// SoA row access: uniform row base (SGPRs) + a 32-bit per-lane byte offset, so loads and
+// stores use the global_load/store saddr form with one shared offset VGPR instead of a
+// 64-bit address per access.  Callers keep b * sizeof(T) < 2^32 (per-launch batch cap).
+template <typename T>
+__device__ __forceinline__ T ld_row(const T *__restrict__ base, int64_t row, uint32_t off) {
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base + row) + off);
+}
+template <typename T>
+__device__ __forceinline__ void st_row(T *__restrict__ base, int64_t row, uint32_t off, T v) {
+    *reinterpret_cast<T *>(reinterpret_cast<char *>(base + row) + off) = v;
+}
+
+// Compiler-only fence: forces per-link constants to be re-read from LDS in a later
+// sweep instead of being kept live in VGPRs across the whole chain.
+__device__ __forceinline__ void reload_fence() { asm volatile("" ::: "memory"); }
+
+// ---------------------------------------------------------------------------- sincos
+// Joint angles need sin/cos once per link.  The ROCm device-library sincos carries a
+// Payne-Hanek branch for huge arguments that inflates every unrolled kernel's register
+// footprint (fp64 7-DOF RNEA: 256 VGPR + 123 AGPR, 1 wave/SIMD).  These are
+// branch-free: Cody-Waite reduction by pi/2 with a 3-term FMA split, then the fdlibm
+// __kernel_sin/__kernel_cos minimax polynomials on |r| <= pi/4 (<= 1 ulp for
+// |x| < 2^20 rad -- far beyond any joint angle).  FAST=true (fp32 only) uses the
+// hardware v_sin_f32/v_cos_f32.
+__device__ __forceinline__ void sincos_cw(double x, double &s, double &c) {
+    const double k = __builtin_rint(x * 6.36619772367581382433e-01);  // 2/pi
+    double r = __builtin_fma(-k, 1.57079632679489655800e+00, x);      // pi/2 hi
+    r = __builtin_fma(-k, 6.12323399573676603587e-17, r);              // pi/2 mid
+    r = __builtin_fma(-k, -1.49738490485916983e-33, r);                // pi/2 lo
+    const double z = r * r;
+    const double v = z * r;
+    const double ps = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+                          1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                          2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                          8.33333333332248946124e-03);
+    const double sr = __builtin_fma(v, __builtin_fma(z, ps, -1.66666666666666324348e-01), r);
+    const double pc = z * __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+                          __builtin_fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                          -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                          -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * pc);
+    const int q = (int)(long long)k & 3;
+    const double ss = (q & 1) ? cr : sr;
+    const double cc = (q & 1) ? sr : cr;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
+}
+
+__device__ __forceinline__ void sincos_cw(float x, float &s, float &c) {
+    const float k = __builtin_rintf(x * 6.3661977236e-01f);
+    float r = __builtin_fmaf(-k, 1.57079637e+00f, x);
+    r = __builtin_fmaf(-k, -4.37113883e-08f, r);
+    r = __builtin_fmaf(-k, -1.71512451e-15f, r);
+    const float z = r * r;
+    const float sr = __builtin_fmaf(z * r, __builtin_fmaf(z, __builtin_fmaf(z, -1.9515295891e-4f,
+                                    8.3321608736e-3f), -1.6666654611e-1f), r);
+    const float cr = __builtin_fmaf(z * z, __builtin_fmaf(z, __builtin_fmaf(z, 2.443315711809948e-5f,
+                                    -1.388731625493765e-3f), 4.166664568298827e-2f), __builtin_fmaf(-0.5f, z, 1.0f));
+    const int q = (int)k & 3;
+    const float ss = (q & 1) ? cr : sr;
+    const float cc = (q & 1) ? sr : cr;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void sin_cos(float x, float &s, float &c) {
+    if constexpr (FAST) {
+        __sincosf(x, &s, &c);
+    } else {
+        sincos_cw(x, s, c);
+    }
+}
+template <bool FAST>
+__device__ __forceinline__ void sin_cos(double x, double &s, double &c) {
+    sincos_cw(x, s, c);
+}
+
+}  // namespace dev
+}  // namespace rbamd

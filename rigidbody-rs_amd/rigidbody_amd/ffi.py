@@ -1,0 +1,329 @@
+"""ctypes binding of librigidbody_bindings.so (include/rigidbody.h + rigidbody_batch.h).
+
+Host-side mirror of the reference's interface for the hot path:
+
+* `Multibody.new()` / `.from_urdf(path)` / `.from_urdf_string(xml)` <- `multibody_new`,
+  `Multibody::from_urdf` (rigidbody_bindings/src/lib.rs:8-12, multibody.rs:65-77)
+* `.rnea(q, dq, ddq)`, `.crba(q)`, `.fwd_kin(q)`, `.jac(q)` <- the single-config C ABI
+  (lib.rs:15-70), same argument meaning and result layout; computed on the GPU
+* `.rnea_batch`, `.fd_batch`, `.crba_batch`, `.fwd_kin_batch`, `.jac_batch` <- batched
+  device-pointer entry points on torch CUDA tensors laid out [n, B] (SoA)
+
+Errors: the reference panics (aborting across FFI) on a bad URDF, a wrong DOF or a
+NULL handle; here every failure raises RigidBodyError with the library's message.
+
+torch is imported before the library is loaded on purpose: torch ships its own
+libamdhip64.so.7 and the dynamic loader then binds this library to that same
+runtime (same SONAME), so torch tensors, streams and these kernels share one HIP
+runtime.  There is no CPU fallback: if the library is missing this import fails.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("RIGIDBODY_AMD_LIB", os.path.join(_PKG, "librigidbody_bindings.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} not found: build the HIP library first (python -c 'import __graft_entry__ as g; g.build()' "
+        "or make -C rigidbody-rs_amd)")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+
+# exported symbols declared in include/*.h (tests check the list against the headers)
+REFERENCE_SYMBOLS = ["multibody_new", "multibody_fwd_kin", "multibody_jac", "multibody_rnea",
+                     "multibody_crba", "multibody_free"]
+
+
+def _sig(name, restype, argtypes):
+    f = getattr(_lib, name)
+    f.restype = restype
+    f.argtypes = argtypes
+    return f
+
+
+_sig("multibody_new", _vp, [])
+_sig("multibody_free", None, [_vp])
+for _n in ("multibody_fwd_kin", "multibody_jac", "multibody_crba"):
+    _sig(_n, _dp, [_vp, _dp])
+_sig("multibody_rnea", _dp, [_vp, _dp, _dp, _dp])
+_sig("multibody_new_from_urdf", _vp, [ctypes.c_char_p])
+_sig("multibody_new_from_urdf_string", _vp, [ctypes.c_char_p, ctypes.c_size_t])
+_sig("multibody_blob_size", _i64, [_vp])
+_sig("multibody_export_blob", ctypes.c_int, [_vp, _dp, _i64])
+_sig("multibody_new_from_blob", _vp, [_dp, _i64])
+_sig("multibody_dof", ctypes.c_int, [_vp])
+_sig("multibody_total_mass", ctypes.c_double, [_vp])
+_sig("multibody_limits", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp])
+_sig("multibody_supported_dofs", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int])
+_sig("multibody_upload", ctypes.c_int, [_vp])
+_sig("multibody_result_free", None, [_dp])
+_sig("rb_last_error", ctypes.c_char_p, [])
+_sig("rb_version", ctypes.c_char_p, [])
+for _t in ("f32", "f64"):
+    _sig(f"multibody_rnea_batch_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp])
+    _sig(f"multibody_fd_batch_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp])
+    _sig(f"multibody_crba_batch_{_t}", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
+    _sig(f"rb_fill_uniform_{_t}", ctypes.c_int, [_vp, ctypes.c_int, _i64, _i64, _dp, _dp, ctypes.c_uint64, _vp])
+_sig("multibody_fwd_kin_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
+_sig("multibody_jac_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
+_sig("multibody_rnea_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
+_sig("multibody_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
+
+
+class RigidBodyError(RuntimeError):
+    pass
+
+
+def last_error() -> str:
+    return (_lib.rb_last_error() or b"").decode()
+
+
+def version() -> str:
+    return _lib.rb_version().decode()
+
+
+def lib():
+    return _lib
+
+
+def supported_dofs():
+    buf = (ctypes.c_int * 64)()
+    n = _lib.multibody_supported_dofs(buf, 64)
+    return [buf[i] for i in range(n)]
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RigidBodyError(f"{what} failed (status {rc}): {last_error()}")
+
+
+def _dvec(x, n):
+    a = np.ascontiguousarray(x, dtype=np.float64)
+    if a.shape != (n,):
+        raise ValueError(f"expected {n} values, got shape {a.shape}")
+    return a
+
+
+def _take(ptr, count):
+    if not ptr:
+        raise RigidBodyError(last_error())
+    out = np.ctypeslib.as_array(ptr, shape=(count,)).copy()
+    _lib.multibody_result_free(ptr)
+    return out
+
+
+_TORCH_SUFFIX = {torch.float32: "f32", torch.float64: "f64"}
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _soa(t, n, name, dtype=None, B=None):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) torch tensor of shape [n, B]")
+    if t.dim() != 2 or t.shape[0] != n:
+        raise ValueError(f"{name} must have shape [{n}, B], got {tuple(t.shape)}")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} has dtype {t.dtype}, expected {dtype}")
+    if B is not None and t.shape[1] != B:
+        raise ValueError(f"{name} has batch {t.shape[1]}, expected {B}")
+    if t.stride(1) != 1:
+        raise ValueError(f"{name} must be contiguous along the batch axis")
+    return t
+
+
+class Multibody:
+    """Handle to a loaded serial chain (reference: `Multibody`, multibody.rs:32)."""
+
+    def __init__(self, handle):
+        if not handle:
+            raise RigidBodyError(last_error())
+        self._h = ctypes.c_void_p(handle)
+        self.n = _lib.multibody_dof(self._h)
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def new(cls):
+        """multibody_new(): $RIGIDBODY_URDF, else the embedded FR3 model."""
+        return cls(_lib.multibody_new())
+
+    @classmethod
+    def from_urdf(cls, path):
+        return cls(_lib.multibody_new_from_urdf(os.fsencode(path)))
+
+    @classmethod
+    def from_urdf_string(cls, xml: str):
+        b = xml.encode()
+        return cls(_lib.multibody_new_from_urdf_string(b, len(b)))
+
+    @classmethod
+    def from_blob(cls, blob):
+        a = np.ascontiguousarray(blob, dtype=np.float64)
+        return cls(_lib.multibody_new_from_blob(a.ctypes.data_as(_dp), a.size))
+
+    def blob(self) -> np.ndarray:
+        size = _lib.multibody_blob_size(self._h)
+        out = np.zeros(size, dtype=np.float64)
+        _check(_lib.multibody_export_blob(self._h, out.ctypes.data_as(_dp), size), "export_blob")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.multibody_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def total_mass(self) -> float:
+        return _lib.multibody_total_mass(self._h)
+
+    def limits(self):
+        arrs = [np.zeros(self.n) for _ in range(4)]
+        _check(_lib.multibody_limits(self._h, *[a.ctypes.data_as(_dp) for a in arrs]), "limits")
+        return tuple(arrs)  # lower, upper, velocity, effort
+
+    def upload(self):
+        _check(_lib.multibody_upload(self._h), "upload")
+
+    # ------------------------------------------------- single configuration (ABI)
+    def rnea(self, q, dq, ddq) -> np.ndarray:
+        q, dq, ddq = (_dvec(x, self.n) for x in (q, dq, ddq))
+        return _take(_lib.multibody_rnea(self._h, q.ctypes.data_as(_dp), dq.ctypes.data_as(_dp),
+                                         ddq.ctypes.data_as(_dp)), self.n)
+
+    def crba_raw(self, q) -> np.ndarray:
+        """n*n column-major buffer exactly as multibody_crba returns it."""
+        q = _dvec(q, self.n)
+        return _take(_lib.multibody_crba(self._h, q.ctypes.data_as(_dp)), self.n * self.n)
+
+    def crba(self, q) -> np.ndarray:
+        return self.crba_raw(q).reshape(self.n, self.n).T.copy()
+
+    def fwd_kin(self, q) -> np.ndarray:
+        q = _dvec(q, self.n)
+        return _take(_lib.multibody_fwd_kin(self._h, q.ctypes.data_as(_dp)), 3)
+
+    def jac_raw(self, q) -> np.ndarray:
+        q = _dvec(q, self.n)
+        return _take(_lib.multibody_jac(self._h, q.ctypes.data_as(_dp)), 6 * self.n)
+
+    def jac(self, q) -> np.ndarray:
+        return self.jac_raw(q).reshape(self.n, 6).T.copy()
+
+    # ------------------------------------------------------- batched, device [n, B]
+    def rnea_batch(self, q, qd, qdd, out=None, stream=None):
+        q = _soa(q, self.n, "q")
+        B = q.shape[1]
+        qd = _soa(qd, self.n, "qd", q.dtype, B)
+        qdd = _soa(qdd, self.n, "qdd", q.dtype, B)
+        if not (q.stride(0) == qd.stride(0) == qdd.stride(0)):
+            raise ValueError("q, qd, qdd must share the leading dimension")
+        if out is None:
+            out = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
+        _soa(out, self.n, "tau", q.dtype, B)
+        if out.stride(0) != q.stride(0):
+            raise ValueError("out must share the inputs' leading dimension")
+        fn = getattr(_lib, f"multibody_rnea_batch_{_TORCH_SUFFIX[q.dtype]}")
+        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), qdd.data_ptr(), out.data_ptr(), B, q.stride(0),
+                  _stream_ptr(stream)), "rnea_batch")
+        return out
+
+    def fd_batch(self, q, qd, tau, out=None, stream=None):
+        q = _soa(q, self.n, "q")
+        B = q.shape[1]
+        qd = _soa(qd, self.n, "qd", q.dtype, B)
+        tau = _soa(tau, self.n, "tau", q.dtype, B)
+        if not (q.stride(0) == qd.stride(0) == tau.stride(0)):
+            raise ValueError("q, qd, tau must share the leading dimension")
+        if out is None:
+            out = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
+        _soa(out, self.n, "qdd", q.dtype, B)
+        if out.stride(0) != q.stride(0):
+            raise ValueError("out must share the inputs' leading dimension")
+        fn = getattr(_lib, f"multibody_fd_batch_{_TORCH_SUFFIX[q.dtype]}")
+        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), out.data_ptr(), B, q.stride(0),
+                  _stream_ptr(stream)), "fd_batch")
+        return out
+
+    def crba_batch(self, q, out=None, stream=None):
+        q = _soa(q, self.n, "q")
+        B = q.shape[1]
+        if out is None:
+            out = torch.empty((self.n * self.n, q.stride(0)), dtype=q.dtype, device=q.device)[:, :B]
+        fn = getattr(_lib, f"multibody_crba_batch_{_TORCH_SUFFIX[q.dtype]}")
+        if out.stride(0) != q.stride(0) or out.shape != (self.n * self.n, B):
+            raise ValueError("out must be [n*n, B] with the inputs' leading dimension")
+        _check(fn(self._h, q.data_ptr(), out.data_ptr(), B, q.stride(0), _stream_ptr(stream)), "crba_batch")
+        return out
+
+    def fwd_kin_batch(self, q, out=None, stream=None):
+        q = _soa(q, self.n, "q", torch.float64)
+        B = q.shape[1]
+        if out is None:
+            out = torch.empty((3, q.stride(0)), dtype=q.dtype, device=q.device)[:, :B]
+        _check(_lib.multibody_fwd_kin_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, q.stride(0),
+                                                _stream_ptr(stream)), "fwd_kin_batch")
+        return out
+
+    def jac_batch(self, q, out=None, stream=None):
+        q = _soa(q, self.n, "q", torch.float64)
+        B = q.shape[1]
+        if out is None:
+            out = torch.empty((6 * self.n, q.stride(0)), dtype=q.dtype, device=q.device)[:, :B]
+        _check(_lib.multibody_jac_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, q.stride(0),
+                                            _stream_ptr(stream)), "jac_batch")
+        return out
+
+    # -------------------------------------------------------- batched, host [n, B]
+    def rnea_batch_host(self, q, qd, qdd):
+        arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (q, qd, qdd)]
+        B = arrs[0].shape[1]
+        out = np.empty_like(arrs[0])
+        _check(_lib.multibody_rnea_batch_host_f64(self._h, *[a.ctypes.data_as(_dp) for a in arrs],
+                                                  out.ctypes.data_as(_dp), B), "rnea_batch_host")
+        return out
+
+    def fd_batch_host(self, q, qd, tau):
+        arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (q, qd, tau)]
+        B = arrs[0].shape[1]
+        out = np.empty_like(arrs[0])
+        _check(_lib.multibody_fd_batch_host_f64(self._h, *[a.ctypes.data_as(_dp) for a in arrs],
+                                                out.ctypes.data_as(_dp), B), "fd_batch_host")
+        return out
+
+
+def fill_uniform(t, lo, hi, seed, stream=None):
+    """rb_fill_uniform_*: t[j, b] = lo[j] + (hi[j]-lo[j]) * u(seed, j, b) on the device."""
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+        raise TypeError("fill_uniform needs a CUDA tensor [rows, B] contiguous along B")
+    rows, B = t.shape
+    lo = np.ascontiguousarray(lo, dtype=np.float64)
+    hi = np.ascontiguousarray(hi, dtype=np.float64)
+    if lo.shape != (rows,) or hi.shape != (rows,):
+        raise ValueError("lo/hi must have one value per row")
+    fn = getattr(_lib, f"rb_fill_uniform_{_TORCH_SUFFIX[t.dtype]}")
+    _check(fn(t.data_ptr(), rows, B, t.stride(0), lo.ctypes.data_as(_dp), hi.ctypes.data_as(_dp),
+              ctypes.c_uint64(seed), _stream_ptr(stream)), "fill_uniform")
+    return t

@@ -1,0 +1,194 @@
+"""The C-ABI boundary on CPU: library loads, exports every declared symbol, and its
+host-side model loading (URDF -> per-link constants, run once, no GPU) matches the
+oracle's restatement of Multibody::from_urdf (multibody.rs:65-77, joint.rs:53-68).
+No compute entry point is called here -- those need a GPU (test_gpu_parity.py)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO, load_json
+
+HEADERS = [os.path.join(REPO, "include", "rigidbody.h"), os.path.join(REPO, "include", "rigidbody_batch.h")]
+
+
+def declared_functions():
+    names = []
+    for h in HEADERS:
+        txt = open(h).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names += re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w]*\s*\**\s*\**\s*(\w+)\s*\(", txt, flags=re.M)
+    return sorted(set(n for n in names if n.startswith(("multibody_", "rb_"))))
+
+
+@pytest.fixture(scope="module")
+def ffi():
+    from rigidbody_amd import ffi
+
+    return ffi
+
+
+def test_headers_declare_reference_abi():
+    names = declared_functions()
+    for sym in ["multibody_new", "multibody_fwd_kin", "multibody_jac", "multibody_rnea", "multibody_crba",
+                "multibody_free"]:
+        assert sym in names
+    assert len(names) >= 30
+
+
+def test_library_exports_every_declared_symbol(ffi):
+    lib = ffi.lib()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_reference_header_compiles_as_c_and_cpp(tmp_path):
+    """rigidbody.h stays a plain C header (the reference's is C++-only) and links."""
+    import subprocess
+
+    src = tmp_path / "use.c"
+    src.write_text('#include "rigidbody_batch.h"\nint main(void){ Multibody *m = 0; multibody_free(m); return 0; }\n')
+    lib = os.path.join(REPO, "rigidbody-rs_amd")
+    for cc, f in (("gcc", str(src)), ("g++", str(src))):
+        args = [cc, "-x", "c" if cc == "gcc" else "c++", f, "-I", os.path.join(REPO, "include"), "-L", lib,
+                "-lrigidbody_bindings", "-o", str(tmp_path / "a.out")]
+        r = subprocess.run(args, capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+
+
+def test_embedded_fr3_model(ffi):
+    mb = ffi.Multibody.new()
+    assert mb.n == 7
+    assert abs(mb.total_mass - 16.062132) < 1e-12
+    lower, upper, vel, eff = mb.limits()
+    np.testing.assert_array_equal(eff, [87, 87, 87, 87, 12, 12, 12])
+    np.testing.assert_array_equal(lower, [-2.3093, -1.5133, -2.4937, -2.7478, -2.48, 0.8521, -2.6895])
+    np.testing.assert_array_equal(vel, [2.0, 1.0, 1.5, 1.25, 3.0, 1.5, 3.0])
+    mb.close()
+
+
+def _blob_links(blob):
+    n = int(blob[2])
+    return n, blob[4:].reshape(n, 36)
+
+
+def test_model_build_matches_oracle(ffi, fr3_text, oracle_mod):
+    """Product preprocessing (C++) vs oracle preprocessing (C), field by field."""
+    from oracle import urdf_model
+    from rigidbody_amd import chains
+
+    for xml in (fr3_text, chains.synthetic_chain_urdf(30), chains.synthetic_chain_urdf(5)):
+        raw = urdf_model.model_raw_from_urdf(xml)
+        om = oracle_mod.Model(raw)
+        ob = np.frombuffer(ctypes.string_at(om._buf, ctypes.sizeof(om._buf)), dtype=np.float64)
+        nmax = 64  # ORACLE_MAX_DOF; oracle_model = {int n (8 B with padding), arrays...}
+        n = raw["n"]
+        off = 1
+        o_axis = ob[off:off + nmax * 3].reshape(nmax, 3)[:n]; off += nmax * 3
+        o_pq = ob[off:off + nmax * 4].reshape(nmax, 4)[:n]; off += nmax * 4
+        o_pt = ob[off:off + nmax * 3].reshape(nmax, 3)[:n]; off += nmax * 3
+        o_m = ob[off:off + nmax][:n]; off += nmax
+        o_com = ob[off:off + nmax * 3].reshape(nmax, 3)[:n]; off += nmax * 3
+        o_ic = ob[off:off + nmax * 9].reshape(nmax, 9)[:n]; off += nmax * 9
+        o_io = ob[off:off + nmax * 9].reshape(nmax, 9)[:n]
+        mb = ffi.Multibody.from_urdf_string(xml)
+        pn, L = _blob_links(mb.blob())
+        assert pn == n
+        np.testing.assert_array_equal(L[:, 0:3], o_axis)
+        np.testing.assert_allclose(L[:, 3:7], o_pq, rtol=0, atol=2e-16)
+        np.testing.assert_array_equal(L[:, 7:10], o_pt)
+        np.testing.assert_array_equal(L[:, 10], o_m)
+        np.testing.assert_array_equal(L[:, 11:14], o_com)
+        np.testing.assert_array_equal(L[:, 14:23], o_ic)
+        np.testing.assert_allclose(L[:, 23:32], o_io, rtol=1e-15, atol=1e-18)
+        mb.close()
+
+
+def test_blob_round_trip(ffi, fr3_text):
+    a = ffi.Multibody.from_urdf_string(fr3_text)
+    b = ffi.Multibody.from_blob(a.blob())
+    np.testing.assert_array_equal(a.blob(), b.blob())
+    with pytest.raises(ffi.RigidBodyError):
+        ffi.Multibody.from_blob(a.blob()[:-1])
+
+
+def test_urdf_file_and_env(ffi, tmp_path, monkeypatch, fr3_text):
+    from rigidbody_amd import chains
+
+    p = tmp_path / "c3.urdf"
+    p.write_text(chains.synthetic_chain_urdf(3))
+    mb = ffi.Multibody.from_urdf(str(p))
+    assert mb.n == 3
+    monkeypatch.setenv("RIGIDBODY_URDF", str(p))
+    assert ffi.Multibody.new().n == 3
+    ref = "/root/reference/assets/fr3.urdf"
+    if os.path.exists(ref):
+        full = ffi.Multibody.from_urdf(ref)
+        np.testing.assert_array_equal(full.blob(), ffi.Multibody.from_urdf_string(fr3_text).blob())
+
+
+@pytest.mark.parametrize("xml,needle", [
+    ("<robot><link name='a'/>", "XML parse error"),
+    ("<notrobot/>", "not <robot>"),
+    ("<robot><link name='a'/><joint name='j' type='fixed'><parent link='a'/><child link='a'/></joint></robot>",
+     "no non-fixed joint"),
+])
+def test_bad_urdf_raises(ffi, xml, needle):
+    with pytest.raises(ffi.RigidBodyError, match=needle):
+        ffi.Multibody.from_urdf_string(xml)
+
+
+def test_unsupported_axis_and_dof(ffi):
+    from rigidbody_amd import chains
+
+    xml = chains.synthetic_chain_urdf(3).replace('<axis xyz="0 0 1"/>', '<axis xyz="1 0 0"/>', 1)
+    with pytest.raises(ffi.RigidBodyError, match="non-z joint axis"):
+        ffi.Multibody.from_urdf_string(xml)
+    dofs = ffi.supported_dofs()
+    assert 7 in dofs and 30 in dofs
+    bad = next(k for k in range(1, 64) if k not in dofs)
+    with pytest.raises(ffi.RigidBodyError, match="no kernel compiled"):
+        ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(bad))
+
+
+def test_null_handle_paths_do_not_abort(ffi):
+    """The reference unwraps NULL and aborts (lib.rs:22,37,50,64); here NULL comes back."""
+    lib = ffi.lib()
+    q = (ctypes.c_double * 7)()
+    assert not lib.multibody_rnea(None, q, q, q)
+    assert not lib.multibody_crba(None, q)
+    assert not lib.multibody_fwd_kin(None, q)
+    assert not lib.multibody_jac(None, q)
+    lib.multibody_free(None)
+    assert lib.multibody_rnea_batch_f32(None, None, None, None, None, 0, 0, None) == 1
+    assert "NULL" in ffi.last_error()
+
+
+def test_index_pairing_detected(ffi):
+    """A URDF whose index pairing differs from child pairing still loads (the reference
+    pairs by index, multibody.rs:70) -- the product follows the reference."""
+    from oracle import urdf_model
+
+    xml = """<robot name="swap">
+      <link name="l1"><inertial><origin xyz="0 0 0.1"/><mass value="1"/><inertia ixx="1" ixy="0" ixz="0" iyy="1" iyz="0" izz="1"/></inertial></link>
+      <link name="l2"><inertial><origin xyz="0 0 0.2"/><mass value="2"/><inertia ixx="2" ixy="0" ixz="0" iyy="2" iyz="0" izz="2"/></inertial></link>
+      <joint name="j2" type="revolute"><parent link="l1"/><child link="l2"/><axis xyz="0 0 1"/></joint>
+      <joint name="j1" type="revolute"><parent link="world"/><child link="l1"/><axis xyz="0 0 1"/></joint>
+    </robot>"""
+    raw = urdf_model.model_raw_from_urdf(xml)
+    assert not urdf_model.index_pairing_matches_child(raw)
+    mb = ffi.Multibody.from_urdf_string(xml)
+    n, L = _blob_links(mb.blob())
+    assert mb.blob()[3] == 0.0  # pairing flag recorded
+    np.testing.assert_array_equal(L[:, 10], raw["mass"])
+
+
+def test_version(ffi):
+    assert "gfx950" in ffi.version()
+
+
+def test_golden_fixture_is_self_consistent():
+    g = load_json("main_cpp_case.json")
+    assert abs(g["total_mass"] - 16.062132) < 1e-12
