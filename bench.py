@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work budget of the baseline sample")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / forward-dynamics side lines")
+    ap.add_argument("--spinup-ms", type=float, default=300.0,
+                    help="untimed launches before the warmup so the GPU clock reaches steady state")
     return ap.parse_args()
 
 
@@ -98,9 +100,11 @@ def make_sets(mb, B, dtype, kernel, nsets, seed):
     return sets
 
 
-def run_timed(mb, sets, kernel, dtype, steps, warmup, world):
+def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0):
     """Warmup, then exactly `steps` launches bracketed by barrier + synchronize.
-    Per-launch hipEvent pairs on the launch stream give the kernel's device time."""
+    A hipEvent pair on the launch stream around the timed launches gives the average
+    device time per launch (kernel + inter-kernel gap); a short untimed pass with an
+    event pair per launch then isolates the kernel alone for comparison with rocprofv3."""
     lib = ffi.lib()
     suffix = "f32" if dtype == torch.float32 else "f64"
     fn = getattr(lib, f"multibody_{'rnea' if kernel == 'rnea' else 'fd'}_batch_{suffix}")
@@ -110,28 +114,45 @@ def run_timed(mb, sets, kernel, dtype, steps, warmup, world):
     args = [(mb.handle, ins[0].data_ptr(), ins[1].data_ptr(), ins[2].data_ptr(), out.data_ptr(), B, B, sp)
             for ins, out in sets]
     ns = len(args)
+    # spin-up: the clock ramps over the first tens of ms of load
+    t_spin = time.perf_counter()
+    i = 0
+    while (time.perf_counter() - t_spin) * 1e3 < spinup_ms:
+        fn(*args[i % ns])
+        i += 1
+        if i % 64 == 0:
+            torch.cuda.synchronize()
     for i in range(warmup):
         rc = fn(*args[i % ns])
         if rc:
             raise RuntimeError(ffi.last_error())
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e0.record(stream)
     for i in range(steps):
-        ev[i][0].record(stream)
         rc = fn(*args[i % ns])
-        ev[i][1].record(stream)
         if rc:
             raise RuntimeError(ffi.last_error())
+    e1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         torch.distributed.barrier()
     wall = t1 - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    return wall, float(np.mean(kern_ms)), float(np.median(kern_ms))
+    region_ms = e0.elapsed_time(e1) / steps
+    # per-launch event pairs (not part of the timed region)
+    m = min(steps, 50)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(m)]
+    for i in range(m):
+        ev[i][0].record(stream)
+        fn(*args[i % ns])
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    per_launch = [a.elapsed_time(b) for a, b in ev]
+    return wall, region_ms, float(np.median(per_launch))
 
 
 def cpu_baseline(n, B_sample_hint, kernel, cpu_seconds):
@@ -188,7 +209,7 @@ def main():
     per_set = 4 * n * a.batch * esize
     nsets = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / per_set)))
     sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED + 7919 * rank)
-    wall, kern_avg_ms, kern_med_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world)
+    wall, kern_avg_ms, kern_med_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms)
     if world > 1:
         t = torch.tensor([wall], device="cuda", dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -218,11 +239,14 @@ def main():
         "config": {"workload": workload, "kernel": a.kernel, "model": "fr3 7-DOF" if n == 7 else f"chain{n}",
                    "batch_per_gpu": a.batch, "global_batch": a.batch * world, "dof": n,
                    "parallelism": f"dp{world} (independent shards, RCCL model broadcast)",
-                   "input_sets": nsets, "rotated_bytes": nsets * per_set},
+                   "input_sets": nsets, "rotated_bytes": nsets * per_set,
+                   "rnea_kernel": mb.rnea_kernel_path(f64=(a.dtype == "f64")) if a.kernel == "rnea" else "generic"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,
-                     "bytes_per_eval": bytes_per_eval, "kernel_ms_avg": kern_avg_ms, "kernel_ms_median": kern_med_ms},
+                     "bytes_per_eval": bytes_per_eval, "kernel_ms_avg": kern_avg_ms,
+                     "kernel_ms_median_event_pair": kern_med_ms,
+                     "timing": "kernel_ms_avg = hipEvent pair around the timed launches / steps"},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(n, a.batch, a.kernel, a.cpu_seconds)
@@ -236,7 +260,7 @@ def main():
             del sets
             torch.cuda.empty_cache()
             sets = make_sets(mb, a.batch, ds, kern, ns, chains.SEED + 31)
-            w, km, _ = run_timed(mb, sets, kern, ds, max(20, a.steps // 4), 5, 1)
+            w, km, _ = run_timed(mb, sets, kern, ds, max(20, a.steps // 4), 5, 1, 100.0)
             sec[f"{kern}_{dt}"] = {"evals_per_s": a.batch * max(20, a.steps // 4) / w, "kernel_ms_avg": km,
                                    "hbm_frac": 4 * n * es * a.batch / (km * 1e-3) / HBM_PEAK}
         line["secondary"] = sec

@@ -76,9 +76,24 @@ int multibody_supported_dofs(int *out, int cap);
  * the first batched call); call before capturing batched calls into a hipGraph. */
 int multibody_upload(const Multibody *mb);
 
+/* Which RNEA kernel runs for this model on the current device: 1 = model-specialised
+ * kernel compiled at first use by hipRTC, 0 = precompiled generic kernel (also when
+ * hipRTC failed; rb_last_error() then holds the compiler log). */
+int multibody_rnea_kernel_path(const Multibody *mb, int f64);
+/* The generated source of the model-specialised RNEA kernel (returns its length;
+ * copies at most cap-1 bytes + NUL into buf when buf != NULL). */
+int multibody_jit_source(const Multibody *mb, int f64, char *buf, int64_t cap);
+/* hipRTC-compiles that kernel for `arch` (NULL = "gfx950") without a device; returns
+ * the code-object size, or minus an rb_status code (log in rb_last_error()). */
+int64_t multibody_jit_compile(const Multibody *mb, int f64, const char *arch);
+
 void multibody_result_free(double *p);
 const char *rb_last_error(void);
 const char *rb_version(void);
+/* Launch-shape knobs for A/B measurements ("rnea_stream": -1 auto / 0 / 1,
+ * "grid_factor": >=1, "jit": 0/1);
+ * defaults are the tuned values.  Process-wide. */
+int rb_set_tuning(const char *key, int value);
 
 /* ---- batched device-pointer entry points (asynchronous on `stream`) ------------ */
 int multibody_rnea_batch_f32(const Multibody *mb, const float *q, const float *qd,

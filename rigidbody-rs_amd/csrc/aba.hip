@@ -22,18 +22,21 @@ __global__ __launch_bounds__(kBlock) void aba_kernel(const T *__restrict__ gmdl,
                                                      T *__restrict__ qdd, uint32_t B,
                                                      int64_t ld) {
     __shared__ T mdl[N * kLinkStride];
-    stage_model<T, N, kBlock>(gmdl, mdl);
+    ModelStage<T, N, kBlock> st;
+    st.fetch(gmdl);
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
-    if (b >= B) return;
     const uint32_t off = b * (uint32_t)sizeof(T);
-
     T qv[N], qdv[N], tv[N];
+    if (b < B) {
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-        qv[j] = ld_row(q, j * ld, off);
-        qdv[j] = ld_row(qd, j * ld, off);
-        tv[j] = ld_row(tau, j * ld, off);
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q, j * ld, off);
+            qdv[j] = ld_row(qd, j * ld, off);
+            tv[j] = ld_row(tau, j * ld, off);
+        }
     }
+    st.commit(mdl);
+    if (b >= B) return;
 
     T cs[N], sn[N];
     T cw0[N], cw1[N], cv0[N], cv1[N];  // c_i = v_i x (S qd_i): (w.y qd, -w.x qd, 0; v.y qd, -v.x qd, 0)

@@ -21,6 +21,8 @@
 #include "../../include/rigidbody_batch.h"
 #include "kernels.hpp"
 #include "model.hpp"
+#include "tuning.hpp"
+#include "jit.hpp"
 
 #include "fr3_embedded.inc"  // kFr3Urdf: compact FR3 description (tools/gen_fixtures.py)
 
@@ -65,6 +67,9 @@ struct Multibody {
     std::vector<double> pk64;
     mutable std::mutex mu;
     mutable std::map<int, DeviceConsts> dev;
+    // model-specialised hipRTC kernels, keyed by (device, dtype, fast trig, stream form)
+    mutable std::map<std::string, rbamd::JitKernel> jit;
+    mutable std::map<std::string, int> jit_device;
 };
 
 namespace {
@@ -121,6 +126,41 @@ int device_consts(const Multibody *mb, const T **out) {
         *out = reinterpret_cast<const T *>(dc.f64);
     }
     return RB_OK;
+}
+
+// The hipRTC kernel for this model on the current device, or nullptr (generic path).
+const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast) {
+    if (!rbamd::jit_enabled()) return nullptr;
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return nullptr;
+    const bool stream = rbamd::rnea_use_stream(f64, mb->model.n);
+    const bool fst = fast && !f64;
+    const std::string key = std::to_string(d) + (f64 ? ":f64" : ":f32") + (fst ? ":fast" : ":precise") +
+                            (stream ? ":stream" : ":lane");
+    std::lock_guard<std::mutex> lk(mb->mu);
+    auto it = mb->jit.find(key);
+    if (it == mb->jit.end()) {
+        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, rbamd::JitKind::Rnea, f64, fst, stream)).first;
+        mb->jit_device[key] = d;
+    }
+    return it->second.function ? &it->second : nullptr;
+}
+
+template <typename T>
+hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *qdd, T *tau,
+                           uint32_t B, int64_t ld, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig())) {
+        const unsigned full = (B + 255u) / 256u;
+        unsigned g = full;
+        if (jk->stream) {
+            const int f = rbamd::tuning().grid_factor < 1 ? 1 : rbamd::tuning().grid_factor;
+            g = jk->resident * (unsigned)f < full ? jk->resident * (unsigned)f : full;
+        }
+        void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&ld};
+        return hipModuleLaunchKernel(jk->function, g, 1, 1, 256, 1, 1, 0, s, args, nullptr);
+    }
+    return rbamd::launch_rnea<T>(mb->model.n, mdl, q, qd, qdd, tau, B, ld, s, fast_trig());
 }
 
 constexpr int64_t kChunk = int64_t(1) << 28;  // per-launch batch cap: b * sizeof(T) < 2^32
@@ -217,8 +257,8 @@ int rnea_batch(const Multibody *mb, const T *q, const T *qd, const T *qdd, T *ta
     const T *mdl = nullptr;
     if ((rc = device_consts<T>(mb, &mdl))) return rc;
     return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = rbamd::launch_rnea<T>(mb->model.n, mdl, q + b0, qd + b0, qdd + b0, tau + b0, nb, ld,
-                                             (hipStream_t)stream, fast_trig());
+        hipError_t e = launch_rnea_any<T>(mb, mdl, q + b0, qd + b0, qdd + b0, tau + b0, nb, ld,
+                                          (hipStream_t)stream);
         return e == hipSuccess ? RB_OK : hip_err(e, "rnea launch");
     });
 }
@@ -350,6 +390,11 @@ void multibody_free(Multibody *mb) {
         if (kv.second.f32) (void)hipFree(kv.second.f32);
         if (kv.second.f64) (void)hipFree(kv.second.f64);
     }
+    for (auto &kv : mb->jit) {
+        if (!kv.second.module) continue;
+        if (hipSetDevice(mb->jit_device[kv.first]) != hipSuccess) continue;
+        (void)hipModuleUnload(kv.second.module);
+    }
     if (have_cur) (void)hipSetDevice(cur);
     delete mb;
 }
@@ -361,7 +406,7 @@ double *multibody_rnea(const Multibody *mb, const double *q, const double *dq, c
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
         if (rc) return rc;
-        hipError_t e = rbamd::launch_rnea<double>((int)n, mdl, din, din + n, din + 2 * n, dout, 1, 1, s, false);
+        hipError_t e = launch_rnea_any<double>(mb, mdl, din, din + n, din + 2 * n, dout, 1, 1, s);
         return e == hipSuccess ? RB_OK : hip_err(e, "rnea launch");
     });
 }
@@ -460,6 +505,40 @@ int multibody_limits(const Multibody *mb, double *lower, double *upper, double *
 
 int multibody_supported_dofs(int *out, int cap) { return rbamd::supported_dofs(out, cap); }
 
+int multibody_rnea_kernel_path(const Multibody *mb, int f64) {
+    if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
+    if (!rbamd::jit_enabled()) return 0;
+    if (jit_rnea(mb, f64 != 0, fast_trig())) return 1;
+    int d = 0;
+    (void)hipGetDevice(&d);
+    std::lock_guard<std::mutex> lk(mb->mu);
+    for (auto &kv : mb->jit)
+        if (!kv.second.error.empty()) g_last_error = kv.second.error;
+    return 0;
+}
+
+int multibody_jit_source(const Multibody *mb, int f64, char *buf, int64_t cap) {
+    if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
+    const std::string src = rbamd::jit_source(mb->model, rbamd::JitKind::Rnea, f64 != 0, fast_trig() && !f64,
+                                              rbamd::rnea_use_stream(f64 != 0, mb->model.n));
+    if (buf && cap > 0) {
+        const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
+        std::memcpy(buf, src.data(), n);
+        buf[n] = 0;
+    }
+    return (int)src.size();
+}
+
+int64_t multibody_jit_compile(const Multibody *mb, int f64, const char *arch) {
+    if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
+    std::vector<char> code;
+    std::string err;
+    if (!rbamd::jit_compile(mb->model, rbamd::JitKind::Rnea, f64 != 0, fast_trig() && !f64,
+                            rbamd::rnea_use_stream(f64 != 0, mb->model.n), arch ? arch : "gfx950", &code, &err))
+        return -set_err(RB_ERR_HIP, err);
+    return (int64_t)code.size();
+}
+
 int multibody_upload(const Multibody *mb) {
     if (!mb) return set_err(RB_ERR_NULL, "NULL Multibody handle");
     const float *a = nullptr;
@@ -472,6 +551,17 @@ int multibody_upload(const Multibody *mb) {
 void multibody_result_free(double *p) { std::free(p); }
 const char *rb_last_error(void) { return g_last_error.c_str(); }
 const char *rb_version(void) { return RB_VERSION; }
+
+int rb_set_tuning(const char *key, int value) {
+    if (!key) return set_err(RB_ERR_NULL, "NULL key");
+    rbamd::Tuning &t = rbamd::tuning();
+    const std::string k(key);
+    if (k == "rnea_stream") t.rnea_stream = value;
+    else if (k == "grid_factor") t.grid_factor = value;
+    else if (k == "jit") t.jit = value;
+    else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
+    return RB_OK;
+}
 
 // ------------------------------------------------------------- batched (device)
 int multibody_rnea_batch_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,

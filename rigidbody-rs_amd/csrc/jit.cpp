@@ -1,0 +1,140 @@
+// jit.cpp -- see jit.hpp.
+#include "jit.hpp"
+
+#include <hip/hiprtc.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <sstream>
+#include <vector>
+
+#include "jit_sources.inc"  // kJitHeaderNames / kJitHeaderSources (tools/embed_sources.py)
+#include "layout.hpp"
+#include "tuning.hpp"
+
+namespace rbamd {
+
+bool jit_enabled() { return tuning().jit != 0; }
+
+namespace {
+
+double snap(double x) {
+    if (std::fabs(x) < 1e-14) return 0.0;
+    if (std::fabs(x - 1.0) < 1e-14) return 1.0;
+    if (std::fabs(x + 1.0) < 1e-14) return -1.0;
+    return x;
+}
+
+std::string literal(double x, bool f64) {
+    char buf[64];
+    if (x == 0.0) return f64 ? "0.0" : "0.0f";
+    if (f64)
+        std::snprintf(buf, sizeof buf, "%.17g", x);
+    else
+        std::snprintf(buf, sizeof buf, "%.9gf", (double)(float)x);
+    std::string s(buf);
+    // make sure an integral value still reads as a floating literal
+    if (s.find_first_of(".eEn") == std::string::npos) s.insert(f64 ? s.size() : s.size() - 1, ".0");
+    return s;
+}
+
+}  // namespace
+
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream) {
+    (void)kind;
+    std::vector<double> pk = m.pack_f64();
+    for (int i = 0; i < m.n; ++i) {
+        double *c = &pk[(size_t)i * kLinkStride];
+        for (int k = 0; k < 9; ++k) c[kE0 + k] = snap(c[kE0 + k]);
+        for (int k = 0; k < 3; ++k) c[kP + k] = snap(c[kP + k]);
+    }
+    std::ostringstream o;
+    o << "#include \"rnea_body.hip.hpp\"\n";
+    o << "using T = " << (f64 ? "double" : "float") << ";\n";
+    o << "constexpr int N = " << m.n << ";\n";
+    o << "static __device__ constexpr T kModel[" << pk.size() << "] = {\n";
+    for (size_t k = 0; k < pk.size(); ++k) o << "  " << literal(pk[k], f64) << ",\n";
+    o << "};\n";
+    o << "extern \"C\" __global__ __launch_bounds__(256) void rb_jit_kernel(const T *__restrict__ q, "
+         "const T *__restrict__ qd, const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
+    o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+    o << "  if (b >= B) return;\n";
+    const char *F = fast ? "true" : "false";
+    if (stream) {
+        o << "  T qv[N], qdv[N], qddv[N];\n";
+        o << "  rbamd::dev::load_cfg<T, N>(q, qd, qdd, ld, b * (uint32_t)sizeof(T), qv, qdv, qddv);\n";
+        o << "  rbamd::dev::rnea_stream_lane<T, N, " << F
+          << ">(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
+    } else {
+        o << "  rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
+    }
+    o << "}\n";
+    return o.str();
+}
+
+bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream, const std::string &arch,
+                 std::vector<char> *code, std::string *error) {
+    const std::string src = jit_source(m, kind, f64, fast, stream);
+    hiprtcProgram prog = nullptr;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "rb_jit.hip", kJitHeaderCount, kJitHeaderSources,
+                            kJitHeaderNames) != HIPRTC_SUCCESS) {
+        *error = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const std::string arch_opt = "--offload-arch=" + arch;
+    const char *opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffinite-math-only", "-fno-signed-zeros"};
+    hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        *error = std::string("hiprtc compile failed: ") + hiprtcGetErrorString(rc) + "\n" + log;
+        hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    size_t code_size = 0;
+    hiprtcGetCodeSize(prog, &code_size);
+    code->resize(code_size);
+    hiprtcGetCode(prog, code->data());
+    hiprtcDestroyProgram(&prog);
+    return true;
+}
+
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stream) {
+    JitKernel jk;
+    jk.stream = stream;
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+        jk.error = "no HIP device";
+        return jk;
+    }
+    std::vector<char> code;
+    if (!jit_compile(m, kind, f64, fast, stream, prop.gcnArchName, &code, &jk.error)) return jk;
+    hipError_t e = hipModuleLoadData(&jk.module, code.data());
+    if (e != hipSuccess) {
+        jk.error = std::string("hipModuleLoadData: ") + hipGetErrorString(e);
+        jk.module = nullptr;
+        return jk;
+    }
+    e = hipModuleGetFunction(&jk.function, jk.module, "rb_jit_kernel");
+    if (e != hipSuccess) {
+        jk.error = std::string("hipModuleGetFunction: ") + hipGetErrorString(e);
+        (void)hipModuleUnload(jk.module);
+        jk.module = nullptr;
+        jk.function = nullptr;
+        return jk;
+    }
+    if (stream) {
+        int per_cu = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jk.function, 256, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 1;
+        jk.resident = (unsigned)per_cu * (unsigned)prop.multiProcessorCount;
+    }
+    return jk;
+}
+
+}  // namespace rbamd

@@ -1,0 +1,48 @@
+// jit.hpp -- model-specialised kernels compiled at model-load time with hipRTC.
+//
+// The precompiled kernels read the model's per-link constants from LDS, so every
+// rotation entry and offset costs an FMA even when it is 0 or +-1.  URDF joint frames
+// are usually signed axis permutations (rpy in multiples of pi/2) with sparse offsets;
+// compiling the SAME device code (rnea_body.hip.hpp) against the model as a constexpr
+// array lets the compiler fold those constants away (FR3 RNEA: ~1090 -> see DESIGN.md).
+// Rotation/offset entries within 1e-14 of 0 or +-1 are snapped to exactly those values
+// (the reference's own quaternion->matrix round trip leaves 1e-16 residues there), and
+// the module is compiled with -ffinite-math-only -fno-signed-zeros so 0*x and 1*x fold.
+//
+// Any hipRTC failure leaves the precompiled generic kernel in charge (still on the GPU);
+// RB_JIT=0 (or rb_set_tuning("jit", 0)) disables the path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "model.hpp"
+
+namespace rbamd {
+
+enum class JitKind : int { Rnea = 0 };
+
+struct JitKernel {
+    hipModule_t module = nullptr;
+    hipFunction_t function = nullptr;
+    bool stream = false;        // grid-stride form: launch a resident-sized grid
+    unsigned resident = 0;      // resident blocks (occupancy x CUs) for the stream form
+    std::string error;          // non-empty when compilation failed
+};
+
+bool jit_enabled();
+
+// Generated HIP source for one specialised kernel (exposed for tests / inspection).
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream);
+
+// hipRTC compilation only (no device needed): fills `code` with the code object.
+bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream, const std::string &arch,
+                 std::vector<char> *code, std::string *error);
+
+// Compiles and loads the kernel on the current device.  Never throws.
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stream);
+
+}  // namespace rbamd

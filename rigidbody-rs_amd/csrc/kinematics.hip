@@ -113,7 +113,11 @@ __global__ __launch_bounds__(kBlock) void fill_uniform_kernel(T *__restrict__ x,
         const double lo = lohi[2 * j], hi = lohi[2 * j + 1];
         // no FMA contraction: the host reproduction (chains.host_uniform) rounds the
         // product and the sum separately
-        st_row(x, j * ld, off, (T)__dadd_rn(lo, __dmul_rn(hi - lo, r)));
+        {
+#pragma clang fp contract(off)
+            const double prod = (hi - lo) * r;
+            st_row(x, j * ld, off, (T)(lo + prod));
+        }
     }
 }
 

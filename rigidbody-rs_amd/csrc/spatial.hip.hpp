@@ -13,7 +13,17 @@
 //   v x* f = (w x n + v x f,  w x f)                               (spatial.rs:129-134)
 #pragma once
 
+#if defined(__HIPCC_RTC__)
+// hipRTC compiles this header for the model-specialised kernels (jit.cpp); it brings
+// the HIP device builtins itself but not <cstdint>.
+typedef unsigned int uint32_t;
+typedef long long int64_t;
+typedef unsigned long long uint64_t;
+#else
 #include <hip/hip_runtime.h>
+
+#include <cstdint>
+#endif
 
 #include "layout.hpp"
 
@@ -115,11 +125,38 @@ struct Link {
     S3<T> Io;
 };
 
+// Two-phase staging so a block's model fetch overlaps its first joint-value loads:
+// fetch() issues the global loads of the packed block into registers, the caller then
+// issues its own input loads, and commit() writes LDS and joins the block at a barrier
+// that waits for LDS traffic only (lgkmcnt), not for the input loads in flight
+// (__syncthreads() would add vmcnt(0) and serialise the two latencies).
+template <typename T, int N, int BLOCK>
+struct ModelStage {
+    static constexpr int kElems = N * kLinkStride;
+    static constexpr int K = (kElems + BLOCK - 1) / BLOCK;
+    T v[K];
+    __device__ __forceinline__ void fetch(const T *__restrict__ g) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = threadIdx.x + k * BLOCK;
+            v[k] = i < kElems ? g[i] : T(0);
+        }
+    }
+    __device__ __forceinline__ void commit(T *smem) const {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = threadIdx.x + k * BLOCK;
+            if (i < kElems) smem[i] = v[k];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+};
+
 template <typename T, int N, int BLOCK>
 __device__ __forceinline__ void stage_model(const T *__restrict__ mdl, T *smem) {
-#pragma unroll
-    for (int k = threadIdx.x; k < N * kLinkStride; k += BLOCK) smem[k] = mdl[k];
-    __syncthreads();
+    ModelStage<T, N, BLOCK> st;
+    st.fetch(mdl);
+    st.commit(smem);
 }
 
 template <typename T>

@@ -1,0 +1,56 @@
+// tuning.cpp -- see tuning.hpp.
+#include "tuning.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
+
+namespace rbamd {
+
+namespace {
+int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+}  // namespace
+
+Tuning &tuning() {
+    static Tuning t = [] {
+        Tuning x;
+        x.rnea_stream = env_int("RB_RNEA_STREAM", x.rnea_stream);
+        x.grid_factor = env_int("RB_GRID_FACTOR", x.grid_factor);
+        x.jit = env_int("RB_JIT", x.jit);
+        return x;
+    }();
+    return t;
+}
+
+unsigned stream_grid(const void *kfn, int block, unsigned full, int factor) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void *>, unsigned> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return full;
+    unsigned resident = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find({dev, kfn});
+        if (it != cache.end()) {
+            resident = it->second;
+        } else {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, block, 0) != hipSuccess || per_cu < 1)
+                per_cu = 1;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+                cus = 256;
+            resident = (unsigned)per_cu * (unsigned)cus;
+            cache[{dev, kfn}] = resident;
+        }
+    }
+    const unsigned g = resident * (unsigned)(factor < 1 ? 1 : factor);
+    return g < full ? g : full;
+}
+
+}  // namespace rbamd

@@ -1,0 +1,30 @@
+// tuning.hpp -- launch-shape knobs (host side) and resident-grid sizing.
+#pragma once
+
+namespace rbamd {
+
+struct Tuning {
+    // RNEA launch form: 1 grid-stride + register prefetch, 0 one configuration per lane,
+    // -1 auto (measured on MI355X: one-per-lane for fp32 up to 8 DOF, streaming for fp64
+    // and longer chains -- tools/ab_bench.py).
+    int rnea_stream = -1;
+    int grid_factor = 1;  // streaming grid = grid_factor x resident blocks (capped by the batch)
+    int jit = 1;          // 1: model-specialised hipRTC kernels where available (jit.hpp)
+};
+
+// Process-wide knobs, initialised from RB_RNEA_STREAM / RB_GRID_FACTOR / RB_JIT, adjustable through
+// rb_set_tuning() (used by the A/B benchmarks; not needed for normal use).
+Tuning &tuning();
+
+// Blocks for a streaming launch of `kfn`: factor x (resident blocks per CU x CUs) on the
+// current device, never more than `full` (one block per 256 configurations).  Cached per
+// (device, kernel).
+unsigned stream_grid(const void *kfn, int block, unsigned full, int factor);
+
+// The RNEA launch-form policy shared by the precompiled and the hipRTC kernels.
+inline bool rnea_use_stream(bool f64, int n) {
+    const int v = tuning().rnea_stream;
+    return v < 0 ? (f64 || n > 8) : v != 0;
+}
+
+}  // namespace rbamd

@@ -77,6 +77,10 @@ for _t in ("f32", "f64"):
 _sig("multibody_fwd_kin_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_jac_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_rnea_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
+_sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
+_sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, _i64])
+_sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_char_p])
+_sig("rb_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
 _sig("multibody_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
 
 
@@ -100,6 +104,11 @@ def supported_dofs():
     buf = (ctypes.c_int * 64)()
     n = _lib.multibody_supported_dofs(buf, 64)
     return [buf[i] for i in range(n)]
+
+
+def set_tuning(key: str, value: int):
+    """rb_set_tuning: process-wide launch knobs ("rnea_stream", "grid_factor", "jit")."""
+    _check(_lib.rb_set_tuning(key.encode(), int(value)), f"set_tuning({key})")
 
 
 def _check(rc, what):
@@ -140,9 +149,26 @@ def _soa(t, n, name, dtype=None, B=None):
         raise TypeError(f"{name} has dtype {t.dtype}, expected {dtype}")
     if B is not None and t.shape[1] != B:
         raise ValueError(f"{name} has batch {t.shape[1]}, expected {B}")
-    if t.stride(1) != 1:
+    if t.shape[1] > 1 and t.stride(1) != 1:
         raise ValueError(f"{name} must be contiguous along the batch axis")
     return t
+
+
+def _ld(t):
+    """Leading dimension (row stride in elements) of an [n, B] tensor."""
+    if t.shape[1] == 0:
+        return 1
+    ld = t.stride(0) if t.shape[0] > 1 else t.shape[1]
+    if ld < t.shape[1]:
+        raise ValueError("rows of an [n, B] array must not overlap (row stride < B)")
+    return ld
+
+
+def _same_ld(ts):
+    lds = {_ld(t) for t in ts}
+    if len(lds) != 1:
+        raise ValueError("all [n, B] arrays of one call must share the leading dimension")
+    return lds.pop()
 
 
 class Multibody:
@@ -207,6 +233,25 @@ class Multibody:
     def upload(self):
         _check(_lib.multibody_upload(self._h), "upload")
 
+    def rnea_kernel_path(self, f64=False) -> str:
+        """'jit' if the model-specialised hipRTC kernel runs on this device, else 'generic'."""
+        r = _lib.multibody_rnea_kernel_path(self._h, int(bool(f64)))
+        if r < 0:
+            raise RigidBodyError(last_error())
+        return "jit" if r == 1 else "generic"
+
+    def jit_source(self, f64=False) -> str:
+        n = _lib.multibody_jit_source(self._h, int(bool(f64)), None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        _lib.multibody_jit_source(self._h, int(bool(f64)), buf, n + 1)
+        return buf.value.decode()
+
+    def jit_compile(self, f64=False, arch="gfx950") -> int:
+        r = _lib.multibody_jit_compile(self._h, int(bool(f64)), arch.encode())
+        if r < 0:
+            raise RigidBodyError(last_error())
+        return r
+
     # ------------------------------------------------- single configuration (ABI)
     def rnea(self, q, dq, ddq) -> np.ndarray:
         q, dq, ddq = (_dvec(x, self.n) for x in (q, dq, ddq))
@@ -238,15 +283,12 @@ class Multibody:
         B = q.shape[1]
         qd = _soa(qd, self.n, "qd", q.dtype, B)
         qdd = _soa(qdd, self.n, "qdd", q.dtype, B)
-        if not (q.stride(0) == qd.stride(0) == qdd.stride(0)):
-            raise ValueError("q, qd, qdd must share the leading dimension")
         if out is None:
             out = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
         _soa(out, self.n, "tau", q.dtype, B)
-        if out.stride(0) != q.stride(0):
-            raise ValueError("out must share the inputs' leading dimension")
+        ld = _same_ld((q, qd, qdd, out))
         fn = getattr(_lib, f"multibody_rnea_batch_{_TORCH_SUFFIX[q.dtype]}")
-        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), qdd.data_ptr(), out.data_ptr(), B, q.stride(0),
+        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), qdd.data_ptr(), out.data_ptr(), B, ld,
                   _stream_ptr(stream)), "rnea_batch")
         return out
 
@@ -255,15 +297,12 @@ class Multibody:
         B = q.shape[1]
         qd = _soa(qd, self.n, "qd", q.dtype, B)
         tau = _soa(tau, self.n, "tau", q.dtype, B)
-        if not (q.stride(0) == qd.stride(0) == tau.stride(0)):
-            raise ValueError("q, qd, tau must share the leading dimension")
         if out is None:
             out = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
         _soa(out, self.n, "qdd", q.dtype, B)
-        if out.stride(0) != q.stride(0):
-            raise ValueError("out must share the inputs' leading dimension")
+        ld = _same_ld((q, qd, tau, out))
         fn = getattr(_lib, f"multibody_fd_batch_{_TORCH_SUFFIX[q.dtype]}")
-        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), out.data_ptr(), B, q.stride(0),
+        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), out.data_ptr(), B, ld,
                   _stream_ptr(stream)), "fd_batch")
         return out
 
@@ -271,19 +310,19 @@ class Multibody:
         q = _soa(q, self.n, "q")
         B = q.shape[1]
         if out is None:
-            out = torch.empty((self.n * self.n, q.stride(0)), dtype=q.dtype, device=q.device)[:, :B]
+            out = torch.empty((self.n * self.n, _ld(q)), dtype=q.dtype, device=q.device)[:, :B]
         fn = getattr(_lib, f"multibody_crba_batch_{_TORCH_SUFFIX[q.dtype]}")
-        if out.stride(0) != q.stride(0) or out.shape != (self.n * self.n, B):
+        if out.shape != (self.n * self.n, B) or (B > 1 and out.stride(0) != _ld(q)):
             raise ValueError("out must be [n*n, B] with the inputs' leading dimension")
-        _check(fn(self._h, q.data_ptr(), out.data_ptr(), B, q.stride(0), _stream_ptr(stream)), "crba_batch")
+        _check(fn(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q), _stream_ptr(stream)), "crba_batch")
         return out
 
     def fwd_kin_batch(self, q, out=None, stream=None):
         q = _soa(q, self.n, "q", torch.float64)
         B = q.shape[1]
         if out is None:
-            out = torch.empty((3, q.stride(0)), dtype=q.dtype, device=q.device)[:, :B]
-        _check(_lib.multibody_fwd_kin_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, q.stride(0),
+            out = torch.empty((3, _ld(q)), dtype=q.dtype, device=q.device)[:, :B]
+        _check(_lib.multibody_fwd_kin_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q),
                                                 _stream_ptr(stream)), "fwd_kin_batch")
         return out
 
@@ -291,8 +330,8 @@ class Multibody:
         q = _soa(q, self.n, "q", torch.float64)
         B = q.shape[1]
         if out is None:
-            out = torch.empty((6 * self.n, q.stride(0)), dtype=q.dtype, device=q.device)[:, :B]
-        _check(_lib.multibody_jac_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, q.stride(0),
+            out = torch.empty((6 * self.n, _ld(q)), dtype=q.dtype, device=q.device)[:, :B]
+        _check(_lib.multibody_jac_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q),
                                             _stream_ptr(stream)), "jac_batch")
         return out
 
@@ -316,7 +355,7 @@ class Multibody:
 
 def fill_uniform(t, lo, hi, seed, stream=None):
     """rb_fill_uniform_*: t[j, b] = lo[j] + (hi[j]-lo[j]) * u(seed, j, b) on the device."""
-    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dim() != 2 or (t.shape[1] > 1 and t.stride(1) != 1):
         raise TypeError("fill_uniform needs a CUDA tensor [rows, B] contiguous along B")
     rows, B = t.shape
     lo = np.ascontiguousarray(lo, dtype=np.float64)
@@ -324,6 +363,6 @@ def fill_uniform(t, lo, hi, seed, stream=None):
     if lo.shape != (rows,) or hi.shape != (rows,):
         raise ValueError("lo/hi must have one value per row")
     fn = getattr(_lib, f"rb_fill_uniform_{_TORCH_SUFFIX[t.dtype]}")
-    _check(fn(t.data_ptr(), rows, B, t.stride(0), lo.ctypes.data_as(_dp), hi.ctypes.data_as(_dp),
+    _check(fn(t.data_ptr(), rows, B, _ld(t), lo.ctypes.data_as(_dp), hi.ctypes.data_as(_dp),
               ctypes.c_uint64(seed), _stream_ptr(stream)), "fill_uniform")
     return t

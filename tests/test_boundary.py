@@ -192,3 +192,25 @@ def test_version(ffi):
 def test_golden_fixture_is_self_consistent():
     g = load_json("main_cpp_case.json")
     assert abs(g["total_mass"] - 16.062132) < 1e-12
+
+
+def test_jit_source_and_compile(ffi, fr3_text):
+    """The model-specialised RNEA kernel (hipRTC) builds for gfx950 without a device, and
+    its source carries the model with the near-0/+-1 rotation entries snapped."""
+    from rigidbody_amd import chains
+
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    src = mb.jit_source(f64=False)
+    assert "constexpr int N = 7" in src and "rnea_lane" in src
+    assert "0.333000004f" in src  # fr3_joint1 origin z (fr3.urdf:62) as an fp32 literal
+    assert "2.22044605e-16" not in src  # rotation residues snapped to exact 0
+    for f64 in (False, True):
+        assert mb.jit_compile(f64=f64) > 1000
+    c30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
+    assert "rnea_stream_lane" in c30.jit_source(f64=False)  # 30 DOF: streaming form
+    assert c30.jit_compile(f64=False) > 1000
+
+
+def test_set_tuning_rejects_unknown_key(ffi):
+    with pytest.raises(ffi.RigidBodyError, match="unknown tuning key"):
+        ffi.set_tuning("no_such_knob", 1)

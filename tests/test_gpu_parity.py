@@ -5,7 +5,13 @@ Tolerances (stated per test):
   fp64 forward dynamics        |d| <= 1e-9 * cond(H) * (1 + |qdd|), and the torque residual
                                |rnea64(q, qd, qdd_gpu) - tau| <= 1e-8 * (1 + |tau|)
   fp32 rnea                    |d| <= 1e-4 * (1 + |tau|)  (Nm)
-  fp32 forward dynamics        torque residual |rnea64(q, qd, qdd32) - tau| <= 1e-3 * (1 + |tau|)
+  fp32 forward dynamics        forward error |qdd32 - qdd64| <= 20 * eps32 * cond(H) * (1 + |qdd64|)
+                               per configuration, plus the torque residual
+                               |rnea64(q, qd, qdd32) - tau| <= 1e-3 * (1 + |tau|) elementwise for
+                               FR3 and the 12-DOF chain (cond(H) <= 1e4); for the 30-DOF chain
+                               (cond(H) ~ 1e5) norm-wise: max|res| <= 1e-2 * (1 + max|tau|).
+                               An fp32 numpy emulation of the same algorithm reaches 4.9e-3
+                               elementwise there (tools/diag_fd32.py).
 Integer-exact: the device input generator equals its host reproduction bit for bit,
 and the strictly-lower CRBA entries are exactly 0 as in the reference ABI.
 """
@@ -115,7 +121,19 @@ def test_batched_f32_vs_golden(name, ffi, dev, fr3_text):
     _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), tau_ref, 1e-4, "rnea f32")
     qdd32 = mb.fd_batch(q, qd, tin).cpu().numpy().astype(np.float64)
     res = om.rnea_batch(q64, qd64, qdd32) - t64
-    assert (np.abs(res) / (1 + np.abs(t64))).max() <= 1e-3
+    if name.startswith("chain30"):
+        assert (np.abs(res).max(axis=0) / (1 + np.abs(t64).max(axis=0))).max() <= 1e-2
+    else:
+        assert (np.abs(res) / (1 + np.abs(t64))).max() <= 1e-3
+    qdd_ref = om.fd_batch(q64, qd64, t64)
+    Hb = om.crba_batch(q64)
+    n = q64.shape[0]
+    eps32 = float(np.finfo(np.float32).eps)
+    for b in range(q64.shape[1]):
+        Hm = Hb[:, b].reshape(n, n).T
+        cond = np.linalg.cond(np.triu(Hm) + np.triu(Hm, 1).T)
+        err = np.abs(qdd32[:, b] - qdd_ref[:, b]).max() / (1 + np.abs(qdd_ref[:, b]).max())
+        assert err <= 20 * eps32 * cond, (b, err, cond)
     H32 = mb.crba_batch(q).cpu().numpy()
     Href = om.crba_batch(q64)
     _close(H32, Href, 1e-4, "crba f32")
@@ -208,3 +226,25 @@ def test_full_size_properties(ffi, dev, fr3_text):
     tau32 = mb.rnea_batch(x32["q"], x32["qd"], x32["qdd"])
     ref32 = om.rnea_batch(*[x32[k][:, idx].double().cpu().numpy() for k in ("q", "qd", "qdd")])
     _close(tau32[:, idx].cpu().numpy(), ref32, 1e-4, "spot f32")
+
+
+# ------------------------------------------------------------ JIT vs generic
+@pytest.mark.parametrize("name", ["fr3_golden.npz", "chain30_golden.npz"])
+def test_jit_and_generic_kernels_agree(name, ffi, dev, fr3_text):
+    """Both RNEA code paths -- model-specialised (hipRTC) and precompiled generic --
+    meet the oracle tolerance; the JIT path is really taken when enabled."""
+    g = load_npz(name)
+    mb = ffi.Multibody.from_urdf_string(_model_xml(name, fr3_text))
+    om = _oracle(_model_xml(name, fr3_text))
+    try:
+        for jit in (1, 0):
+            ffi.set_tuning("jit", jit)
+            assert mb.rnea_kernel_path(f64=False) == ("jit" if jit else "generic"), ffi.last_error()
+            assert mb.rnea_kernel_path(f64=True) == ("jit" if jit else "generic"), ffi.last_error()
+            q, qd, qdd = (_t(g[k], dev) for k in ("q", "qd", "qdd"))
+            _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), g["tau"], 1e-9, f"rnea f64 jit={jit}")
+            q32, qd32, qdd32 = (x.float() for x in (q, qd, qdd))
+            ref = om.rnea_batch(*[x.double().cpu().numpy() for x in (q32, qd32, qdd32)])
+            _close(mb.rnea_batch(q32, qd32, qdd32).cpu().numpy(), ref, 1e-4, f"rnea f32 jit={jit}")
+    finally:
+        ffi.set_tuning("jit", 1)

@@ -1,0 +1,59 @@
+"""A/B launch-shape comparison inside ONE process (interleaved rounds, median/min),
+per cdna_hip_programming.md §5.4 rule 24.  Times the batched kernels over rotated
+input sets (> Infinity Cache) with a hipEvent pair around `steps` launches.
+
+usage: python tools/ab_bench.py [--kernel rnea|fd] [--dtype f32|f64] [--dof 7]
+                                [--variants 'rnea_stream=0' 'rnea_stream=1,grid_factor=2' ...]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "rigidbody-rs_amd")]
+import bench  # noqa: E402
+from rigidbody_amd import chains, ffi  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="rnea")
+    ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--dof", type=int, default=7)
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", nargs="+", default=["rnea_stream=0", "rnea_stream=1"])
+    a = ap.parse_args()
+    dtype = bench.DT[a.dtype]
+    es = 4 if a.dtype == "f32" else 8
+    mb = ffi.Multibody.new() if a.dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(a.dof))
+    mb.upload()
+    per = 4 * mb.n * a.batch * es
+    nsets = max(2, int(np.ceil(1.25 * (1 << 30) / per)))
+    sets = bench.make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED)
+    lib = ffi.lib()
+    res = {v: [] for v in a.variants}
+    for r in range(a.rounds):
+        for v in a.variants:
+            for kv in v.split(","):
+                k, val = kv.split("=")
+                assert lib.rb_set_tuning(k.encode(), int(val)) == 0, ffi.last_error()
+            _, ms, _ = bench.run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0 if r == 0 else 0.0)
+            res[v].append(ms)
+    out = {}
+    for v, ms in res.items():
+        med = float(np.median(ms))
+        out[v] = {"ms_median": med, "ms_min": float(np.min(ms)),
+                  "evals_per_s": a.batch / (med * 1e-3),
+                  "hbm_frac": 4 * mb.n * es * a.batch / (med * 1e-3) / bench.HBM_PEAK}
+    print(json.dumps({"kernel": a.kernel, "dtype": a.dtype, "dof": a.dof, "batch": a.batch, "results": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
