@@ -94,6 +94,10 @@ const char *rb_version(void);
  * "grid_factor": >=1, "jit": 0/1);
  * defaults are the tuned values.  Process-wide. */
 int rb_set_tuning(const char *key, int value);
+/* Bandwidth probe with the batched kernels' access pattern: reads rows_in SoA rows and
+ * writes rows_out rows of `batch` floats (width 1: 4 B per lane, 4: 16 B per lane). */
+int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
+                      int width, void *stream);
 
 /* ---- batched device-pointer entry points (asynchronous on `stream`) ------------ */
 int multibody_rnea_batch_f32(const Multibody *mb, const float *q, const float *qd,

@@ -133,7 +133,7 @@ const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast) {
     if (!rbamd::jit_enabled()) return nullptr;
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
-    const bool stream = rbamd::rnea_use_stream(f64, mb->model.n);
+    const bool stream = rbamd::rnea_use_stream(f64, mb->model.n, true);
     const bool fst = fast && !f64;
     const std::string key = std::to_string(d) + (f64 ? ":f64" : ":f32") + (fst ? ":fast" : ":precise") +
                             (stream ? ":stream" : ":lane");
@@ -158,7 +158,12 @@ hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const 
             g = jk->resident * (unsigned)f < full ? jk->resident * (unsigned)f : full;
         }
         void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&ld};
-        return hipModuleLaunchKernel(jk->function, g, 1, 1, 256, 1, 1, 0, s, args, nullptr);
+        hipFunction_t fn = jk->function;
+        const auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
+        if (jk->tile_function && rbamd::tuning().rnea_tile && a16(q) && a16(qd) && a16(qdd) && a16(tau) &&
+            ((uint64_t)ld * sizeof(T)) % 16 == 0)
+            fn = jk->tile_function;
+        return hipModuleLaunchKernel(fn, g, 1, 1, 256, 1, 1, 0, s, args, nullptr);
     }
     return rbamd::launch_rnea<T>(mb->model.n, mdl, q, qd, qdd, tau, B, ld, s, fast_trig());
 }
@@ -520,7 +525,7 @@ int multibody_rnea_kernel_path(const Multibody *mb, int f64) {
 int multibody_jit_source(const Multibody *mb, int f64, char *buf, int64_t cap) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
     const std::string src = rbamd::jit_source(mb->model, rbamd::JitKind::Rnea, f64 != 0, fast_trig() && !f64,
-                                              rbamd::rnea_use_stream(f64 != 0, mb->model.n));
+                                              rbamd::rnea_use_stream(f64 != 0, mb->model.n, true));
     if (buf && cap > 0) {
         const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
         std::memcpy(buf, src.data(), n);
@@ -534,7 +539,7 @@ int64_t multibody_jit_compile(const Multibody *mb, int f64, const char *arch) {
     std::vector<char> code;
     std::string err;
     if (!rbamd::jit_compile(mb->model, rbamd::JitKind::Rnea, f64 != 0, fast_trig() && !f64,
-                            rbamd::rnea_use_stream(f64 != 0, mb->model.n), arch ? arch : "gfx950", &code, &err))
+                            rbamd::rnea_use_stream(f64 != 0, mb->model.n, true), arch ? arch : "gfx950", &code, &err))
         return -set_err(RB_ERR_HIP, err);
     return (int64_t)code.size();
 }
@@ -552,6 +557,15 @@ void multibody_result_free(double *p) { std::free(p); }
 const char *rb_last_error(void) { return g_last_error.c_str(); }
 const char *rb_version(void) { return RB_VERSION; }
 
+int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
+                      int width, void *stream) {
+    if (!in || !out) return set_err(RB_ERR_NULL, "NULL array");
+    if (rows_in < 1 || rows_out < 0 || batch < 0 || ld < batch || batch > kChunk || (width != 1 && width != 4))
+        return set_err(RB_ERR_ARG, "bad probe shape");
+    hipError_t e = rbamd::launch_probe_rows(in, out, rows_in, rows_out, (uint32_t)batch, ld, width, (hipStream_t)stream);
+    return e == hipSuccess ? RB_OK : hip_err(e, "probe launch");
+}
+
 int rb_set_tuning(const char *key, int value) {
     if (!key) return set_err(RB_ERR_NULL, "NULL key");
     rbamd::Tuning &t = rbamd::tuning();
@@ -559,6 +573,7 @@ int rb_set_tuning(const char *key, int value) {
     if (k == "rnea_stream") t.rnea_stream = value;
     else if (k == "grid_factor") t.grid_factor = value;
     else if (k == "jit") t.jit = value;
+    else if (k == "rnea_tile") t.rnea_tile = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

@@ -17,6 +17,8 @@ namespace rbamd {
 
 bool jit_enabled() { return tuning().jit != 0; }
 
+bool jit_tile_ok(int n, bool f64) { return 3 * n * 256 * (f64 ? 8 : 4) <= 48 * 1024; }
+
 namespace {
 
 double snap(double x) {
@@ -70,6 +72,18 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         o << "  rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
     }
     o << "}\n";
+    if (jit_tile_ok(m.n, f64)) {
+        o << "extern \"C\" __global__ __launch_bounds__(256) void rb_jit_tile(const T *__restrict__ q, "
+             "const T *__restrict__ qd, const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
+        o << "  __shared__ T tile[3 * N * 256];\n";
+        o << "  const uint32_t b0 = blockIdx.x * 256u;\n";
+        o << "  if (b0 + 256u <= B) {\n";
+        o << "    rbamd::dev::rnea_tile<T, N, " << F << ">(kModel, q, qd, qdd, tau, b0, ld, tile);\n";
+        o << "  } else {\n";
+        o << "    const uint32_t b = b0 + threadIdx.x;\n";
+        o << "    if (b < B) rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
+        o << "  }\n}\n";
+    }
     return o.str();
 }
 
@@ -119,6 +133,8 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stre
         jk.module = nullptr;
         return jk;
     }
+    if (jit_tile_ok(m.n, f64) && hipModuleGetFunction(&jk.tile_function, jk.module, "rb_jit_tile") != hipSuccess)
+        jk.tile_function = nullptr;
     e = hipModuleGetFunction(&jk.function, jk.module, "rb_jit_kernel");
     if (e != hipSuccess) {
         jk.error = std::string("hipModuleGetFunction: ") + hipGetErrorString(e);

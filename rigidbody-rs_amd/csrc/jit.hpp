@@ -27,13 +27,17 @@ enum class JitKind : int { Rnea = 0 };
 
 struct JitKernel {
     hipModule_t module = nullptr;
-    hipFunction_t function = nullptr;
+    hipFunction_t function = nullptr;       // one configuration per lane (any layout)
+    hipFunction_t tile_function = nullptr;  // LDS-tiled, 16-byte global accesses (aligned SoA)
     bool stream = false;        // grid-stride form: launch a resident-sized grid
     unsigned resident = 0;      // resident blocks (occupancy x CUs) for the stream form
     std::string error;          // non-empty when compilation failed
 };
 
 bool jit_enabled();
+
+// The LDS-tiled kernel form is generated when the 3N-row input tile fits in 48 KiB.
+bool jit_tile_ok(int n, bool f64);
 
 // Generated HIP source for one specialised kernel (exposed for tests / inspection).
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream);

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(kBlock) void rnea_kernel(const T *__restrict__ gmdl
     if (b < B) load_cfg<T, N>(q, qd, qdd, ld, off, qv, qdv, qddv);
     st.commit(mdl);
     if (b >= B) return;
-    rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, tau, ld, off);
+    rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
 }
 
 // Streaming form (rnea_stream_lane): resident-sized grid, register prefetch.
@@ -60,7 +60,7 @@ hipError_t rnea_go(const T *mdl, const T *q, const T *qd, const T *qdd, T *tau, 
                    hipStream_t s) {
     const Tuning &tn = tuning();
     const unsigned full = dev::grid_for(B);
-    const bool stream = rnea_use_stream(sizeof(T) == 8, N);
+    const bool stream = rnea_use_stream(sizeof(T) == 8, N, false);
     auto kfn = stream ? dev::rnea_stream_kernel<T, N, F> : dev::rnea_kernel<T, N, F>;
     const unsigned g = stream ? stream_grid((const void *)kfn, dev::kBlock, full, tn.grid_factor) : full;
     hipLaunchKernelGGL(kfn, dim3(g), dim3(dev::kBlock), 0, s, mdl, q, qd, qdd, tau, B, ld);

@@ -11,11 +11,10 @@ namespace dev {
 // ----------------------------------------------------------------------------- RNEA
 // Forward sweep (multibody.rs:122-141) then backward sweep (143-150), fused: the
 // per-link forces never leave registers.  One call evaluates the configuration whose
-// joint values are in (qv, qdv, qddv) and stores its torques at byte offset `off`.
-template <typename T, int N, bool FAST>
+// joint values are in (qv, qdv, qddv) and hands tau_j to `out(j, value)`.
+template <typename T, int N, bool FAST, typename Out>
 __device__ __forceinline__ void rnea_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
-                                          const T (&qddv)[N], T *__restrict__ tau, int64_t ld,
-                                          uint32_t off) {
+                                          const T (&qddv)[N], Out &&out) {
     T cs[N], sn[N];
     V3<T> fn[N], ff[N];  // per-link spatial force: moment n (rot), force f (lin)
     V3<T> w, v, aw, av;  // link velocity / acceleration (rot, lin), link coordinates
@@ -68,7 +67,7 @@ __device__ __forceinline__ void rnea_eval(const T *mdl, const T (&qv)[N], const 
     reload_fence();
 #pragma unroll
     for (int j = N - 1; j >= 1; --j) {
-        st_row(tau, j * ld, off, fn[j].z);
+        out(j, fn[j].z);
         const T *c = mdl + j * kLinkStride;
         const M3<T> Rp{{c[kE0 + 0], c[kE0 + 1], c[kE0 + 2], c[kE0 + 3], c[kE0 + 4], c[kE0 + 5],
                         c[kE0 + 6], c[kE0 + 7], c[kE0 + 8]}};
@@ -81,7 +80,7 @@ __device__ __forceinline__ void rnea_eval(const T *mdl, const T (&qv)[N], const 
         ff[j - 1] = v3(ff[j - 1].x + fl.x, ff[j - 1].y + fl.y, ff[j - 1].z + fl.z);
         fn[j - 1] = cross_add(mul_add(fn[j - 1], Rp, zn), p, fl);
     }
-    st_row(tau, 0, off, fn[0].z);
+    out(0, fn[0].z);
 }
 
 template <typename T, int N>
@@ -104,7 +103,7 @@ __device__ __forceinline__ void rnea_lane(const T *mdl, const T *__restrict__ q,
     const uint32_t off = b * (uint32_t)sizeof(T);
     T qv[N], qdv[N], qddv[N];
     load_cfg<T, N>(q, qd, qdd, ld, off, qv, qdv, qddv);
-    rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, tau, ld, off);
+    rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
 }
 
 // Streaming form: walk the batch with `stride`, prefetching the next configuration's
@@ -120,7 +119,8 @@ __device__ __forceinline__ void rnea_stream_lane(const T *mdl, const T *__restri
         const bool more = bn < B;
         T nq[N], nqd[N], nqdd[N];
         if (more) load_cfg<T, N>(q, qd, qdd, ld, bn * (uint32_t)sizeof(T), nq, nqd, nqdd);
-        rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, tau, ld, b * (uint32_t)sizeof(T));
+        const uint32_t off = b * (uint32_t)sizeof(T);
+        rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
         if (!more) break;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -130,6 +130,83 @@ __device__ __forceinline__ void rnea_stream_lane(const T *mdl, const T *__restri
         }
         b = bn;
     }
+}
+
+// ------------------------------------------------------------------ LDS-tiled form
+// A 256-thread block owns configurations [b0, b0+256).  Global traffic moves whole tile
+// rows with 16-byte accesses (one 1 KiB wave-instruction per fp32 row; the probe in
+// probe.hip measures 4-byte lanes at 3.8-3.9 TB/s vs 5.0-5.5 TB/s for 16-byte lanes on
+// this pattern), and the per-lane math keeps one configuration per lane reading its
+// values from LDS (conflict-free: lane t reads word t of a row).
+template <typename T>
+struct Vec16;
+template <>
+struct Vec16<float> {
+    using type = float4;
+};
+template <>
+struct Vec16<double> {
+    using type = double2;
+};
+
+constexpr int kTile = 256;
+
+template <typename T, int ROWS>
+__device__ __forceinline__ void tile_load(const T *__restrict__ a0, const T *__restrict__ a1,
+                                          const T *__restrict__ a2, int rows_per_array, int64_t ld,
+                                          uint32_t b0, T *tile) {
+    using V = typename Vec16<T>::type;
+    constexpr int VPL = 16 / (int)sizeof(T);  // values per 16-byte access
+    constexpr int LPR = kTile / VPL;          // accesses per tile row
+#pragma unroll
+    for (int k0 = 0; k0 < ROWS * LPR; k0 += kTile) {
+        const int k = k0 + (int)threadIdx.x;
+        if (k < ROWS * LPR) {
+            const int r = k / LPR, c = k % LPR;
+            const int arr = r / rows_per_array, j = r % rows_per_array;
+            const T *base = arr == 0 ? a0 : (arr == 1 ? a1 : a2);
+            const V v = *reinterpret_cast<const V *>(base + j * ld + b0 + c * VPL);
+            *reinterpret_cast<V *>(tile + r * kTile + c * VPL) = v;
+        }
+    }
+}
+
+template <typename T, int ROWS>
+__device__ __forceinline__ void tile_store(T *__restrict__ dst, int64_t ld, uint32_t b0, const T *tile) {
+    using V = typename Vec16<T>::type;
+    constexpr int VPL = 16 / (int)sizeof(T);
+    constexpr int LPR = kTile / VPL;
+#pragma unroll
+    for (int k0 = 0; k0 < ROWS * LPR; k0 += kTile) {
+        const int k = k0 + (int)threadIdx.x;
+        if (k < ROWS * LPR) {
+            const int r = k / LPR, c = k % LPR;
+            *reinterpret_cast<V *>(dst + r * ld + b0 + c * VPL) =
+                *reinterpret_cast<const V *>(tile + r * kTile + c * VPL);
+        }
+    }
+}
+
+// Whole-block tile: caller guarantees b0 + 256 <= B and 16-byte alignment of every row
+// start (base pointers and ld * sizeof(T) multiples of 16).  `tile` holds 3N rows.
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void rnea_tile(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                          const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b0,
+                                          int64_t ld, T *tile) {
+    const int t = (int)threadIdx.x;
+    tile_load<T, 3 * N>(q, qd, qdd, N, ld, b0, tile);
+    __syncthreads();
+    T qv[N], qdv[N], qddv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qv[j] = tile[j * kTile + t];
+        qdv[j] = tile[(N + j) * kTile + t];
+        qddv[j] = tile[(2 * N + j) * kTile + t];
+    }
+    __syncthreads();  // every lane holds its inputs; rows 0..N-1 become the output tile
+    rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, [&](int j, T v) { tile[j * kTile + t] = v; });
+    __syncthreads();
+    tile_store<T, N>(tau, ld, b0, tile);
 }
 
 }  // namespace dev

@@ -23,6 +23,7 @@ Tuning &tuning() {
         x.rnea_stream = env_int("RB_RNEA_STREAM", x.rnea_stream);
         x.grid_factor = env_int("RB_GRID_FACTOR", x.grid_factor);
         x.jit = env_int("RB_JIT", x.jit);
+        x.rnea_tile = env_int("RB_RNEA_TILE", x.rnea_tile);
         return x;
     }();
     return t;

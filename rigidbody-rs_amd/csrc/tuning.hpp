@@ -10,6 +10,7 @@ struct Tuning {
     int rnea_stream = -1;
     int grid_factor = 1;  // streaming grid = grid_factor x resident blocks (capped by the batch)
     int jit = 1;          // 1: model-specialised hipRTC kernels where available (jit.hpp)
+    int rnea_tile = 1;    // 1: LDS-tiled 16-byte-access form of the JIT RNEA kernel when aligned
 };
 
 // Process-wide knobs, initialised from RB_RNEA_STREAM / RB_GRID_FACTOR / RB_JIT, adjustable through
@@ -21,10 +22,13 @@ Tuning &tuning();
 // (device, kernel).
 unsigned stream_grid(const void *kfn, int block, unsigned full, int factor);
 
-// The RNEA launch-form policy shared by the precompiled and the hipRTC kernels.
-inline bool rnea_use_stream(bool f64, int n) {
+// RNEA launch form.  Measured (tools/ab_bench.py): for the precompiled
+// generic kernels the streaming form wins for fp64 and chains longer than 8 links; the
+// model-specialised (JIT) kernels are lighter and the one-per-lane form wins everywhere.
+inline bool rnea_use_stream(bool f64, int n, bool jit) {
     const int v = tuning().rnea_stream;
-    return v < 0 ? (f64 || n > 8) : v != 0;
+    if (v >= 0) return v != 0;
+    return jit ? false : (f64 || n > 8);
 }
 
 }  // namespace rbamd

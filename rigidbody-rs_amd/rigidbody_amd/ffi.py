@@ -81,6 +81,7 @@ _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
 _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_char_p])
 _sig("rb_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
+_sig("rb_probe_rows_f32", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _i64, _i64, ctypes.c_int, _vp])
 _sig("multibody_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
 
 

@@ -207,7 +207,7 @@ def test_jit_source_and_compile(ffi, fr3_text):
     for f64 in (False, True):
         assert mb.jit_compile(f64=f64) > 1000
     c30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
-    assert "rnea_stream_lane" in c30.jit_source(f64=False)  # 30 DOF: streaming form
+    assert "rnea_lane" in c30.jit_source(f64=False)  # JIT kernels use the one-per-lane form
     assert c30.jit_compile(f64=False) > 1000
 
 

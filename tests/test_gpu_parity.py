@@ -237,14 +237,39 @@ def test_jit_and_generic_kernels_agree(name, ffi, dev, fr3_text):
     mb = ffi.Multibody.from_urdf_string(_model_xml(name, fr3_text))
     om = _oracle(_model_xml(name, fr3_text))
     try:
-        for jit in (1, 0):
+        for jit, tile in ((1, 1), (1, 0), (0, 1)):
             ffi.set_tuning("jit", jit)
+            ffi.set_tuning("rnea_tile", tile)
             assert mb.rnea_kernel_path(f64=False) == ("jit" if jit else "generic"), ffi.last_error()
             assert mb.rnea_kernel_path(f64=True) == ("jit" if jit else "generic"), ffi.last_error()
             q, qd, qdd = (_t(g[k], dev) for k in ("q", "qd", "qdd"))
-            _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), g["tau"], 1e-9, f"rnea f64 jit={jit}")
+            _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), g["tau"], 1e-9, f"rnea f64 jit={jit} tile={tile}")
             q32, qd32, qdd32 = (x.float() for x in (q, qd, qdd))
             ref = om.rnea_batch(*[x.double().cpu().numpy() for x in (q32, qd32, qdd32)])
-            _close(mb.rnea_batch(q32, qd32, qdd32).cpu().numpy(), ref, 1e-4, f"rnea f32 jit={jit}")
+            _close(mb.rnea_batch(q32, qd32, qdd32).cpu().numpy(), ref, 1e-4, f"rnea f32 jit={jit} tile={tile}")
     finally:
         ffi.set_tuning("jit", 1)
+        ffi.set_tuning("rnea_tile", 1)
+
+
+def test_tiled_kernel_partial_tiles_and_alignment(ffi, dev, fr3_text):
+    """The LDS-tiled JIT form: batches that end mid-tile, a misaligned leading dimension
+    (falls back to the per-lane form), and offset views all match the oracle."""
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    om = _oracle(fr3_text)
+    rng = np.random.default_rng(11)
+    for B, ld in ((256, 256), (300, 300), (1000, 1003), (513, 1024), (4096 + 77, 4096 + 80)):
+        full = [_t(rng.uniform(-2, 2, (7, ld)), dev) for _ in range(3)]
+        ins = [f[:, :B] for f in full]
+        out = torch.empty((7, ld), dtype=torch.float64, device=dev)[:, :B]
+        mb.rnea_batch(*ins, out=out)
+        _close(out.cpu().numpy(), om.rnea_batch(*[x.cpu().numpy() for x in ins]), 1e-9, f"B={B} ld={ld}")
+        # fp32, including a view that starts 1 element in (misaligned base pointer)
+        f32 = [f.float() for f in full]
+        for start in (0, 1):
+            if start + B > ld:
+                continue
+            ins32 = [f[:, start:start + B] for f in f32]
+            got = mb.rnea_batch(*ins32).cpu().numpy()
+            ref = om.rnea_batch(*[x.double().cpu().numpy() for x in ins32])
+            _close(got, ref, 1e-4, f"f32 B={B} ld={ld} start={start}")
