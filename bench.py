@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work budget of the baseline sample")
     ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / forward-dynamics side lines")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the consecutive batches rotate over (1 = strictly serial launches)")
     ap.add_argument("--spinup-ms", type=float, default=300.0,
                     help="untimed launches before the warmup so the GPU clock reaches steady state")
     return ap.parse_args()
@@ -100,59 +102,63 @@ def make_sets(mb, B, dtype, kernel, nsets, seed):
     return sets
 
 
-def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0):
+def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1):
     """Warmup, then exactly `steps` launches bracketed by barrier + synchronize.
-    A hipEvent pair on the launch stream around the timed launches gives the average
-    device time per launch (kernel + inter-kernel gap); a short untimed pass with an
-    event pair per launch then isolates the kernel alone for comparison with rocprofv3."""
+    Consecutive batches are issued round-robin on `streams` HIP streams (independent
+    batches; the next launch fills the CUs the previous one's tail leaves idle).  Every
+    timed launch is bracketed by its own hipEvent pair on the stream it runs on (the
+    per-kernel duration rocprofv3 also reports); one more pair spans the whole region.
+    Returns (wall s, region ms per launch, mean per-launch kernel ms)."""
     lib = ffi.lib()
     suffix = "f32" if dtype == torch.float32 else "f64"
     fn = getattr(lib, f"multibody_{'rnea' if kernel == 'rnea' else 'fd'}_batch_{suffix}")
-    stream = torch.cuda.current_stream()
-    sp = ctypes.c_void_p(stream.cuda_stream)
+    main = torch.cuda.current_stream()
+    strs = [main] + [torch.cuda.Stream() for _ in range(streams - 1)]
     B = sets[0][1].shape[1]
-    args = [(mb.handle, ins[0].data_ptr(), ins[1].data_ptr(), ins[2].data_ptr(), out.data_ptr(), B, B, sp)
-            for ins, out in sets]
+    args = [[(mb.handle, ins[0].data_ptr(), ins[1].data_ptr(), ins[2].data_ptr(), out.data_ptr(), B, B,
+              ctypes.c_void_p(st.cuda_stream)) for st in strs] for ins, out in sets]
     ns = len(args)
     # spin-up: the clock ramps over the first tens of ms of load (DESIGN.md §5)
     t_spin = time.perf_counter()
     i = 0
     while (time.perf_counter() - t_spin) * 1e3 < spinup_ms:
-        fn(*args[i % ns])
+        fn(*args[i % ns][i % streams])
         i += 1
         if i % 64 == 0:
             torch.cuda.synchronize()
     for i in range(warmup):
-        rc = fn(*args[i % ns])
+        rc = fn(*args[i % ns][i % streams])
         if rc:
             raise RuntimeError(ffi.last_error())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    ends = [torch.cuda.Event() for _ in strs]
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record(stream)
+    e0.record(main)
+    for st in strs[1:]:
+        st.wait_event(e0)
     for i in range(steps):
-        rc = fn(*args[i % ns])
+        st = strs[i % streams]
+        ev[i][0].record(st)
+        rc = fn(*args[i % ns][i % streams])
+        ev[i][1].record(st)
         if rc:
             raise RuntimeError(ffi.last_error())
-    e1.record(stream)
+    for st, end in zip(strs[1:], ends[1:]):
+        end.record(st)
+        main.wait_event(end)
+    e1.record(main)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         torch.distributed.barrier()
     wall = t1 - t0
     region_ms = e0.elapsed_time(e1) / steps
-    # per-launch event pairs (not part of the timed region)
-    m = min(steps, 50)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(m)]
-    for i in range(m):
-        ev[i][0].record(stream)
-        fn(*args[i % ns])
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
     per_launch = [a.elapsed_time(b) for a, b in ev]
-    return wall, region_ms, float(np.median(per_launch))
+    return wall, region_ms, float(np.mean(per_launch))
 
 
 def cpu_baseline(n, B_sample_hint, kernel, cpu_seconds):
@@ -209,18 +215,20 @@ def main():
     per_set = 4 * n * a.batch * esize
     nsets = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / per_set)))
     sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED + 7919 * rank)
-    wall, kern_avg_ms, kern_med_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms)
+    wall, region_ms, kern_avg_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms,
+                                             a.streams)
     if world > 1:
         t = torch.tensor([wall], device="cuda", dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         wall = t.item()
-        k = torch.tensor([kern_avg_ms], device="cuda", dtype=torch.float64)
+        k = torch.tensor([kern_avg_ms, region_ms], device="cuda", dtype=torch.float64)
         torch.distributed.all_reduce(k, op=torch.distributed.ReduceOp.MAX)
-        kern_avg_ms = k.item()
+        kern_avg_ms, region_ms = k.tolist()
     evals = world * a.batch * a.steps
     value = evals / wall
     bytes_per_eval = 4 * n * esize  # q, qd, qdd|tau read + tau|qdd written
-    achieved = bytes_per_eval * a.batch / (kern_avg_ms * 1e-3)
+    achieved = bytes_per_eval * a.batch / (kern_avg_ms * 1e-3)   # per kernel (rocprofv3-comparable)
+    effective = bytes_per_eval * a.batch / (region_ms * 1e-3)    # per step, overlapped launches
     workload = f"{'rnea' if a.kernel == 'rnea' else 'fd'}_{'fr3' if n == 7 else f'chain{n}'}_{a.dtype}_b{a.batch}"
     traffic = load_traffic(workload)
     line = {
@@ -237,6 +245,7 @@ def main():
         "dtype": a.dtype,
         "data": "synthetic (device splitmix64, SURVEY.md §8(d) distributions, seed 20250224)",
         "config": {"workload": workload, "kernel": a.kernel, "model": "fr3 7-DOF" if n == 7 else f"chain{n}",
+                   "streams": a.streams,
                    "batch_per_gpu": a.batch, "global_batch": a.batch * world, "dof": n,
                    "parallelism": f"dp{world} (independent shards, RCCL model broadcast)",
                    "input_sets": nsets, "rotated_bytes": nsets * per_set,
@@ -244,9 +253,12 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,
-                     "bytes_per_eval": bytes_per_eval, "kernel_ms_avg": kern_avg_ms,
-                     "kernel_ms_median_event_pair": kern_med_ms,
-                     "timing": "kernel_ms_avg = hipEvent pair around the timed launches / steps"},
+                     "bytes_per_eval": bytes_per_eval, "launches_per_step": 1,
+                     "kernel_ms_avg": kern_avg_ms, "step_ms_device": region_ms,
+                     "effective_GBps": effective / 1e9, "effective_frac": effective / HBM_PEAK,
+                     "timing": ("kernel_ms_avg = mean of per-launch hipEvent pairs on each launch's stream in the "
+                                "timed region (= rocprofv3 kernel duration); step_ms_device = event pair around all "
+                                f"{a.steps} launches / steps with {a.streams} stream(s)")},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(n, a.batch, a.kernel, a.cpu_seconds)
@@ -260,9 +272,11 @@ def main():
             del sets
             torch.cuda.empty_cache()
             sets = make_sets(mb, a.batch, ds, kern, ns, chains.SEED + 31)
-            w, km, _ = run_timed(mb, sets, kern, ds, max(20, a.steps // 4), 5, 1, 100.0)
+            w, rm, km = run_timed(mb, sets, kern, ds, max(20, a.steps // 4), 5, 1, 100.0, a.streams)
             sec[f"{kern}_{dt}"] = {"evals_per_s": a.batch * max(20, a.steps // 4) / w, "kernel_ms_avg": km,
-                                   "hbm_frac": 4 * n * es * a.batch / (km * 1e-3) / HBM_PEAK}
+                                   "step_ms_device": rm,
+                                   "hbm_frac_kernel": 4 * n * es * a.batch / (km * 1e-3) / HBM_PEAK,
+                                   "hbm_frac_effective": 4 * n * es * a.batch / (rm * 1e-3) / HBM_PEAK}
         line["secondary"] = sec
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -95,7 +95,8 @@ const char *rb_version(void);
  * defaults are the tuned values.  Process-wide. */
 int rb_set_tuning(const char *key, int value);
 /* Bandwidth probe with the batched kernels' access pattern: reads rows_in SoA rows and
- * writes rows_out rows of `batch` floats (width 1: 4 B per lane, 4: 16 B per lane). */
+ * writes rows_out rows of `batch` floats (width 1/2/4: 4/8/16 B per lane; + 16 * nt with
+ * nt bit 0 = non-temporal loads, bit 1 = non-temporal stores). */
 int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
                       int width, void *stream);
 

@@ -136,7 +136,7 @@ const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast) {
     const bool stream = rbamd::rnea_use_stream(f64, mb->model.n, true);
     const bool fst = fast && !f64;
     const std::string key = std::to_string(d) + (f64 ? ":f64" : ":f32") + (fst ? ":fast" : ":precise") +
-                            (stream ? ":stream" : ":lane");
+                            (stream ? ":stream" : ":lane") + ":nt" + std::to_string(rbamd::tuning().rnea_nt & 3);
     std::lock_guard<std::mutex> lk(mb->mu);
     auto it = mb->jit.find(key);
     if (it == mb->jit.end()) {
@@ -560,7 +560,7 @@ const char *rb_version(void) { return RB_VERSION; }
 int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
                       int width, void *stream) {
     if (!in || !out) return set_err(RB_ERR_NULL, "NULL array");
-    if (rows_in < 1 || rows_out < 0 || batch < 0 || ld < batch || batch > kChunk || (width != 1 && width != 4))
+    if (rows_in < 1 || rows_out < 0 || batch < 0 || ld < batch || batch > kChunk || ((width & 15) != 1 && (width & 15) != 2 && (width & 15) != 4) || (width >> 4) > 3)
         return set_err(RB_ERR_ARG, "bad probe shape");
     hipError_t e = rbamd::launch_probe_rows(in, out, rows_in, rows_out, (uint32_t)batch, ld, width, (hipStream_t)stream);
     return e == hipSuccess ? RB_OK : hip_err(e, "probe launch");
@@ -574,6 +574,7 @@ int rb_set_tuning(const char *key, int value) {
     else if (k == "grid_factor") t.grid_factor = value;
     else if (k == "jit") t.jit = value;
     else if (k == "rnea_tile") t.rnea_tile = value;
+    else if (k == "rnea_nt") t.rnea_nt = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

@@ -52,6 +52,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         for (int k = 0; k < 3; ++k) c[kP + k] = snap(c[kP + k]);
     }
     std::ostringstream o;
+    o << "#define RB_NT " << (tuning().rnea_nt & 3) << "\n";
     o << "#include \"rnea_body.hip.hpp\"\n";
     o << "using T = " << (f64 ? "double" : "float") << ";\n";
     o << "constexpr int N = " << m.n << ";\n";

@@ -1,7 +1,7 @@
 // probe.hip -- bandwidth probe with the RNEA access pattern (rows_in SoA rows read,
 // rows_out rows written, no dynamics).  It measures the HBM ceiling the batched kernels
-// can reach with a given per-lane access width: 4 B (one configuration per lane, what the
-// kernels do) or 16 B (four consecutive configurations per lane).  Also used to calibrate
+// can reach with a given per-lane access width: 4 B (one fp32 configuration per lane, what
+// the kernels do), 8 B or 16 B (two / four consecutive configurations per lane).  Also used to calibrate
 // rocprofv3 FETCH_SIZE / WRITE_SIZE against a known byte count.
 #include <hip/hip_runtime.h>
 
@@ -20,35 +20,83 @@ struct VecOf<1> {
     using type = float;
 };
 template <>
+struct VecOf<2> {
+    using type = float __attribute__((ext_vector_type(2)));
+};
+template <>
 struct VecOf<4> {
-    using type = float4;
+    using type = float __attribute__((ext_vector_type(4)));
 };
 
-template <int W>
+// All RI loads of a lane are issued before any use (compile-time row counts), as in the
+// unrolled dynamics kernels.
+template <int W, int RI, int RO, int NT>
 __global__ __launch_bounds__(kBlock) void probe_rows_kernel(const float *__restrict__ in, float *__restrict__ out,
-                                                           int rows_in, int rows_out, uint32_t B, int64_t ld) {
+                                                           uint32_t B, int64_t ld) {
     using V = typename VecOf<W>::type;
     const uint32_t b = (blockIdx.x * kBlock + threadIdx.x) * W;
     if (b >= B) return;
-    V acc{};
-    for (int r = 0; r < rows_in; ++r) acc = acc + *reinterpret_cast<const V *>(in + r * ld + b);
-    for (int r = 0; r < rows_out; ++r) *reinterpret_cast<V *>(out + r * ld + b) = acc;
+    V x[RI];
+#pragma unroll
+    for (int r = 0; r < RI; ++r) {
+        const V *p = reinterpret_cast<const V *>(in + r * ld + b);
+        x[r] = (NT & 1) ? __builtin_nontemporal_load(p) : *p;
+    }
+    V acc = x[0];
+#pragma unroll
+    for (int r = 1; r < RI; ++r) acc = acc + x[r];
+#pragma unroll
+    for (int r = 0; r < RO; ++r) {
+        V *p = reinterpret_cast<V *>(out + r * ld + b);
+        if (NT & 2)
+            __builtin_nontemporal_store(acc, p);
+        else
+            *p = acc;
+    }
 }
 
 }  // namespace dev
 
+namespace {
+template <int RI, int RO, int NT>
+hipError_t probe_go(const float *in, float *out, uint32_t B, int64_t ld, int width, hipStream_t s) {
+    if (width == 4) {
+        hipLaunchKernelGGL((dev::probe_rows_kernel<4, RI, RO, NT>), dim3(dev::grid_for(B / 4)), dim3(dev::kBlock), 0,
+                           s, in, out, B, ld);
+    } else if (width == 2) {
+        hipLaunchKernelGGL((dev::probe_rows_kernel<2, RI, RO, NT>), dim3(dev::grid_for(B / 2)), dim3(dev::kBlock), 0,
+                           s, in, out, B, ld);
+    } else {
+        hipLaunchKernelGGL((dev::probe_rows_kernel<1, RI, RO, NT>), dim3(dev::grid_for(B)), dim3(dev::kBlock), 0, s,
+                           in, out, B, ld);
+    }
+    return hipGetLastError();
+}
+
+template <int RI, int RO>
+hipError_t probe_nt(const float *in, float *out, uint32_t B, int64_t ld, int width, int nt, hipStream_t s) {
+    switch (nt) {
+        case 1: return probe_go<RI, RO, 1>(in, out, B, ld, width, s);
+        case 2: return probe_go<RI, RO, 2>(in, out, B, ld, width, s);
+        case 3: return probe_go<RI, RO, 3>(in, out, B, ld, width, s);
+        default: return probe_go<RI, RO, 0>(in, out, B, ld, width, s);
+    }
+}
+}  // namespace
+
+// Row shapes of the dynamics kernels: 7-DOF (21 in / 7 out), 12-DOF, 30-DOF, and 4/4.
 hipError_t launch_probe_rows(const float *in, float *out, int rows_in, int rows_out, uint32_t B, int64_t ld,
                              int width, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    if (width == 4) {
-        if (B % 4 != 0 || ld % 4 != 0) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(dev::probe_rows_kernel<4>, dim3(dev::grid_for(B / 4)), dim3(dev::kBlock), 0, s, in, out,
-                           rows_in, rows_out, B, ld);
-    } else {
-        hipLaunchKernelGGL(dev::probe_rows_kernel<1>, dim3(dev::grid_for(B)), dim3(dev::kBlock), 0, s, in, out,
-                           rows_in, rows_out, B, ld);
-    }
-    return hipGetLastError();
+    // width encodes the non-temporal flags above the access width: width = w + 16*nt
+    const int nt = width >> 4;
+    width &= 15;
+    if (B % width != 0 || ld % width != 0) return hipErrorInvalidValue;
+    if (rows_in == 21 && rows_out == 7) return probe_nt<21, 7>(in, out, B, ld, width, nt, s);
+    if (rows_in == 36 && rows_out == 12) return probe_nt<36, 12>(in, out, B, ld, width, nt, s);
+    if (rows_in == 90 && rows_out == 30) return probe_nt<90, 30>(in, out, B, ld, width, nt, s);
+    if (rows_in == 4 && rows_out == 4) return probe_nt<4, 4>(in, out, B, ld, width, nt, s);
+    return hipErrorInvalidValue;
 }
 
 }  // namespace rbamd

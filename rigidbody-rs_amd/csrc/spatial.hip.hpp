@@ -197,13 +197,25 @@ __device__ __forceinline__ void inertia_mul(const Link<T> &L, const V3<T> &w, co
 // SoA row access: uniform row base (SGPRs) + a 32-bit per-lane byte offset, so loads and
 // stores use the global_load/store saddr form with one shared offset VGPR instead of a
 // 64-bit address per access.  Callers keep b * sizeof(T) < 2^32 (per-launch batch cap).
+// RB_NT (set by the hipRTC source, jit.cpp): bit 0 non-temporal row loads, bit 1
+// non-temporal row stores -- every input/output element is touched exactly once.
+#ifndef RB_NT
+#define RB_NT 0
+#endif
 template <typename T>
 __device__ __forceinline__ T ld_row(const T *__restrict__ base, int64_t row, uint32_t off) {
-    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base + row) + off);
+    const T *p = reinterpret_cast<const T *>(reinterpret_cast<const char *>(base + row) + off);
+    if constexpr ((RB_NT & 1) != 0) return __builtin_nontemporal_load(p);
+    return *p;
 }
 template <typename T>
 __device__ __forceinline__ void st_row(T *__restrict__ base, int64_t row, uint32_t off, T v) {
-    *reinterpret_cast<T *>(reinterpret_cast<char *>(base + row) + off) = v;
+    T *p = reinterpret_cast<T *>(reinterpret_cast<char *>(base + row) + off);
+    if constexpr ((RB_NT & 2) != 0) {
+        __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
 }
 
 // Compiler-only fence: forces per-link constants to be re-read from LDS in a later

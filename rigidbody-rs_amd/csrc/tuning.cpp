@@ -24,6 +24,7 @@ Tuning &tuning() {
         x.grid_factor = env_int("RB_GRID_FACTOR", x.grid_factor);
         x.jit = env_int("RB_JIT", x.jit);
         x.rnea_tile = env_int("RB_RNEA_TILE", x.rnea_tile);
+        x.rnea_nt = env_int("RB_RNEA_NT", x.rnea_nt);
         return x;
     }();
     return t;

@@ -10,7 +10,13 @@ struct Tuning {
     int rnea_stream = -1;
     int grid_factor = 1;  // streaming grid = grid_factor x resident blocks (capped by the batch)
     int jit = 1;          // 1: model-specialised hipRTC kernels where available (jit.hpp)
-    int rnea_tile = 1;    // 1: LDS-tiled 16-byte-access form of the JIT RNEA kernel when aligned
+    // 1: LDS-tiled 16-byte-access form of the JIT RNEA kernel when aligned.  Off: it is
+    // 30% slower than the per-lane form on MI355X (block barriers serialise load/compute/
+    // store; the per-lane form already runs at the pattern's copy ceiling).
+    int rnea_tile = 0;
+    // JIT RNEA: bit 0 non-temporal loads, bit 1 non-temporal stores (every element is
+    // touched once; measured -5% fp32 / -8% fp64 kernel time).
+    int rnea_nt = 3;
 };
 
 // Process-wide knobs, initialised from RB_RNEA_STREAM / RB_GRID_FACTOR / RB_JIT, adjustable through

@@ -28,7 +28,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", nargs="+", default=["rnea_stream=0", "rnea_stream=1"])
+    ap.add_argument("--variants", nargs="+", default=["rnea_stream=0", "rnea_stream=1"],
+                    help="comma-separated rb_set_tuning key=value lists; the pseudo-key 'streams' "
+                         "sets how many HIP streams the timed launches rotate over")
     a = ap.parse_args()
     dtype = bench.DT[a.dtype]
     es = 4 if a.dtype == "f32" else 8
@@ -41,10 +43,14 @@ def main():
     res = {v: [] for v in a.variants}
     for r in range(a.rounds):
         for v in a.variants:
+            nstreams = 1
             for kv in v.split(","):
                 k, val = kv.split("=")
+                if k == "streams":
+                    nstreams = int(val)
+                    continue
                 assert lib.rb_set_tuning(k.encode(), int(val)) == 0, ffi.last_error()
-            _, ms, _ = bench.run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0 if r == 0 else 0.0)
+            _, ms, _kern = bench.run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
             res[v].append(ms)
     out = {}
     for v, ms in res.items():

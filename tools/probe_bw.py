@@ -14,14 +14,14 @@ sys.path[:0] = [REPO, os.path.join(REPO, "rigidbody-rs_amd")]
 from rigidbody_amd import ffi  # noqa: E402
 
 
-def run(rows_in, rows_out, width, B=1 << 20, steps=100, rounds=5):
+def run(rows_in, rows_out, width, nt=0, B=1 << 20, steps=100, rounds=5):
     per = (rows_in + rows_out) * B * 4
     nsets = max(2, int(np.ceil(1.25 * (1 << 30) / per)))
     sets = [(torch.rand((rows_in, B), device="cuda"), torch.empty((max(rows_out, 1), B), device="cuda"))
             for _ in range(nsets)]
     lib = ffi.lib()
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    args = [(i.data_ptr(), o.data_ptr(), rows_in, rows_out, B, B, width, sp) for i, o in sets]
+    args = [(i.data_ptr(), o.data_ptr(), rows_in, rows_out, B, B, width + 16 * nt, sp) for i, o in sets]
     for k in range(200):
         assert lib.rb_probe_rows_f32(*args[k % nsets]) == 0, ffi.last_error()
     ms = []
@@ -34,10 +34,10 @@ def run(rows_in, rows_out, width, B=1 << 20, steps=100, rounds=5):
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1) / steps)
     med = float(np.median(ms))
-    return {"rows_in": rows_in, "rows_out": rows_out, "width_bytes": 4 * width, "us": med * 1e3,
+    return {"rows_in": rows_in, "rows_out": rows_out, "width_bytes": 4 * width, "nt": nt, "us": med * 1e3,
             "TBps": (rows_in + rows_out) * B * 4 / (med * 1e-3) / 1e12}
 
 
 if __name__ == "__main__":
-    out = [run(21, 7, 1), run(21, 7, 4), run(90, 30, 1), run(90, 30, 4), run(4, 4, 4)]
+    out = [run(ri, ro, w, nt) for ri, ro in ((21, 7), (90, 30), (4, 4)) for w in (1, 4) for nt in (0, 1, 2, 3)]
     print(json.dumps(out, indent=1))
