@@ -50,7 +50,7 @@ def main():
                     nstreams = int(val)
                     continue
                 assert lib.rb_set_tuning(k.encode(), int(val)) == 0, ffi.last_error()
-            _, ms, _kern = bench.run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
+            _, ms = bench.run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
             res[v].append(ms)
     out = {}
     for v, ms in res.items():
