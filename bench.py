@@ -27,6 +27,7 @@ for _p in (REPO, os.path.join(REPO, "rigidbody-rs_amd")):
         sys.path.insert(0, _p)
 
 from rigidbody_amd import chains, ffi  # noqa: E402
+from rigidbody_amd import dist as rdist  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (/opt/skills/guides/MI355X_MICROARCH.md)
 DT = {"f32": torch.float32, "f64": torch.float64}
@@ -54,34 +55,32 @@ def parse():
 
 
 def init_dist():
+    """One process per GPU (torch.distributed.run).  Backend "nccl" = RCCL over xGMI;
+    RB_DIST_BACKEND=gloo rehearses the multi-process path with several ranks sharing
+    one GPU (ranks map to devices round-robin)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local % ndev)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("RB_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local % ndev))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
 def load_model(world, rank, dof):
-    """Rank 0 parses the URDF; the packed fp64 model blob is broadcast over RCCL."""
-    import torch.distributed as dist
+    """Rank 0 parses the URDF; the packed fp64 model blob is broadcast over RCCL
+    (rigidbody_amd.dist.broadcast_model)."""
+    def make():
+        return ffi.Multibody.new() if dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(dof))
 
-    if rank == 0:
-        mb = ffi.Multibody.new() if dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(dof))
-        blob = torch.as_tensor(mb.blob(), device="cuda")
-        size = torch.tensor([blob.numel()], device="cuda", dtype=torch.int64)
-    else:
-        size = torch.zeros(1, device="cuda", dtype=torch.int64)
-    if world > 1:
-        dist.broadcast(size, 0)
-        if rank != 0:
-            blob = torch.empty(int(size.item()), device="cuda", dtype=torch.float64)
-        dist.broadcast(blob, 0)
-        if rank != 0:
-            mb = ffi.Multibody.from_blob(blob.cpu().numpy())
+    mb = rdist.broadcast_model(make, rank, world, torch.device("cuda"))
     mb.upload()
     return mb
 
@@ -208,15 +207,9 @@ def main():
     mb = load_model(world, rank, n)
     per_set = 4 * n * a.batch * esize
     nsets = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / per_set)))
-    sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED + 7919 * rank)
+    sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, rdist.rank_seed(chains.SEED, rank))
     wall, kern_avg_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms, a.streams)
-    if world > 1:
-        t = torch.tensor([wall], device="cuda", dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        wall = t.item()
-        k = torch.tensor([kern_avg_ms], device="cuda", dtype=torch.float64)
-        torch.distributed.all_reduce(k, op=torch.distributed.ReduceOp.MAX)
-        kern_avg_ms = k.item()
+    wall, kern_avg_ms = rdist.max_over_ranks([wall, kern_avg_ms], world, torch.device("cuda"))
     evals = world * a.batch * a.steps
     value = evals / wall
     bytes_per_eval = 4 * n * esize  # q, qd, qdd|tau read + tau|qdd written
