@@ -273,3 +273,27 @@ def test_tiled_kernel_partial_tiles_and_alignment(ffi, dev, fr3_text):
             got = mb.rnea_batch(*ins32).cpu().numpy()
             ref = om.rnea_batch(*[x.double().cpu().numpy() for x in ins32])
             _close(got, ref, 1e-4, f"f32 B={B} ld={ld} start={start}")
+
+
+# ------------------------------------------------------------ drop-in consumer
+def test_cpp_consumer_drop_in(tmp_path, dev):
+    """examples/main_drop_in.cpp (the reference consumer's rigidbody calls) compiled against
+    include/rigidbody.h and linked to librigidbody_bindings.so, run as its own process."""
+    import os
+    import subprocess
+
+    from conftest import PKG, REPO
+
+    exe = tmp_path / "main_drop_in"
+    r = subprocess.run(["g++", "-O2", os.path.join(REPO, "examples", "main_drop_in.cpp"), "-I",
+                        os.path.join(REPO, "include"), "-L", PKG, "-lrigidbody_bindings",
+                        f"-Wl,-rpath,{PKG}", "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = {l.split()[0]: [float(v) for v in l.split()[1:]] for l in r.stdout.splitlines() if l}
+    g = load_json("main_cpp_case.json")["cases"]["main_cpp"]
+    _close(lines["tau"], g["tau"], 1e-9, "consumer tau")
+    _close(lines["pos"], g["fwd_kin"], 1e-9, "consumer fwd_kin")
+    _close(lines["jac"], g["jac_raw"], 1e-9, "consumer jac")
+    _close(lines["crba"], g["crba_raw"], 1e-9, "consumer crba")
