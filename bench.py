@@ -234,7 +234,7 @@ def main():
                    "batch_per_gpu": a.batch, "global_batch": a.batch * world, "dof": n,
                    "parallelism": f"dp{world} (independent shards, RCCL model broadcast)",
                    "input_sets": nsets, "rotated_bytes": nsets * per_set,
-                   "rnea_kernel": mb.rnea_kernel_path(f64=(a.dtype == "f64")) if a.kernel == "rnea" else "generic"},
+                   "kernel_path": mb.kernel_path(a.kernel, f64=(a.dtype == "f64"))},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,

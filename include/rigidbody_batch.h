@@ -76,16 +76,17 @@ int multibody_supported_dofs(int *out, int cap);
  * the first batched call); call before capturing batched calls into a hipGraph. */
 int multibody_upload(const Multibody *mb);
 
-/* Which RNEA kernel runs for this model on the current device: 1 = model-specialised
- * kernel compiled at first use by hipRTC, 0 = precompiled generic kernel (also when
- * hipRTC failed; rb_last_error() then holds the compiler log). */
+/* Which kernel runs for this model on the current device; kind 0 = rnea, 1 = fd,
+ * 2 = crba.  1 = model-specialised kernel compiled at first use by hipRTC, 0 =
+ * precompiled generic kernel (also when hipRTC failed; rb_last_error() holds the log). */
+int multibody_kernel_path(const Multibody *mb, int kind, int f64);
 int multibody_rnea_kernel_path(const Multibody *mb, int f64);
-/* The generated source of the model-specialised RNEA kernel (returns its length;
- * copies at most cap-1 bytes + NUL into buf when buf != NULL). */
-int multibody_jit_source(const Multibody *mb, int f64, char *buf, int64_t cap);
+/* The generated source of a model-specialised kernel (returns its length; copies at
+ * most cap-1 bytes + NUL into buf when buf != NULL). */
+int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap);
 /* hipRTC-compiles that kernel for `arch` (NULL = "gfx950") without a device; returns
  * the code-object size, or minus an rb_status code (log in rb_last_error()). */
-int64_t multibody_jit_compile(const Multibody *mb, int f64, const char *arch);
+int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char *arch);
 
 void multibody_result_free(double *p);
 const char *rb_last_error(void);

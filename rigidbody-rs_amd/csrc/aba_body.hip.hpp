@@ -1,0 +1,138 @@
+// aba_body.hip.hpp -- per-lane forward dynamics by the Articulated-Body Algorithm
+// (device).  Shared by the precompiled kernels (aba.hip) and the model-specialised
+// hipRTC kernels (jit.cpp).  Featherstone Table 7.1 with z-axis joints (S = rot z) and
+// the reference's fictitious-gravity base acceleration (0, +g) (multibody.rs:117-120);
+// defines qdd = sym(H)^-1 (tau - rnea(q, qd, 0)) with H from Multibody::crba
+// (multibody.rs:155-174) -- the reference has no forward-dynamics solve.
+#pragma once
+
+#include "artinertia.hip.hpp"
+
+namespace rbamd {
+namespace dev {
+
+template <typename T, int N, bool FAST, typename Out>
+__device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
+                                         Out &&out) {
+    T cs[N], sn[N];
+    T cw0[N], cw1[N], cv0[N], cv1[N];  // c_i = v_i x (S qd_i): (w.y qd, -w.x qd, 0; v.y qd, -v.x qd, 0)
+    V3<T> pn[N], pf[N];                // bias force p_i = v_i x* (I_i v_i)
+
+    // Pass 1: velocities and bias terms.
+    V3<T> w = v3(T(0), T(0), T(0)), v = v3(T(0), T(0), T(0));
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const Link<T> L = load_link(mdl, j);
+        sin_cos<FAST>(qv[j], sn[j], cs[j]);
+        const T qdj = qdv[j];
+        if (j == 0) {
+            w = v3(T(0), T(0), qdj);
+            v = v3(T(0), T(0), T(0));
+        } else {
+            const M3<T> E = joint_rotation(L.Rp, cs[j], sn[j]);
+            const V3<T> u = cross_sub(v, L.p, w);
+            w = mul_t(E, w);
+            v = mul_t(E, u);
+            w.z += qdj;
+        }
+        cw0[j] = w.y * qdj; cw1[j] = -w.x * qdj;
+        cv0[j] = v.y * qdj; cv1[j] = -v.x * qdj;
+        V3<T> In, If;
+        inertia_mul(L, w, v, In, If);
+        pf[j] = cross(w, If);
+        pn[j] = cross_add(cross(w, In), v, If);
+    }
+
+    // Pass 2: articulated inertias, leaf to root.
+    reload_fence();
+    T Ur[N][3], Ul[N][3], invD[N], uu[N];
+    ArtI<T> IA = rigid_inertia(load_link(mdl, N - 1));
+    V3<T> pAn = pn[N - 1], pAf = pf[N - 1];
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) {
+        const V3<T> ur = v3(IA.A.xz, IA.A.yz, IA.A.zz);
+        const V3<T> ul = v3(IA.B.m[6], IA.B.m[7], IA.B.m[8]);
+        const T Dinv = T(1) / IA.A.zz;
+        const T u = tv[j] - pAn.z;
+        Ur[j][0] = ur.x; Ur[j][1] = ur.y; Ur[j][2] = ur.z;
+        Ul[j][0] = ul.x; Ul[j][1] = ul.y; Ul[j][2] = ul.z;
+        invD[j] = Dinv;
+        uu[j] = u;
+        if (j > 0) {
+            const V3<T> dr = v3(ur.x * Dinv, ur.y * Dinv, ur.z * Dinv);
+            const V3<T> dl = v3(ul.x * Dinv, ul.y * Dinv, ul.z * Dinv);
+            // Ia = IA - U U^T / D
+            ArtI<T> Ia;
+            Ia.A = S3<T>{fmadd(-dr.x, ur.x, IA.A.xx), fmadd(-dr.x, ur.y, IA.A.xy), fmadd(-dr.x, ur.z, IA.A.xz),
+                         fmadd(-dr.y, ur.y, IA.A.yy), fmadd(-dr.y, ur.z, IA.A.yz), fmadd(-dr.z, ur.z, IA.A.zz)};
+            const T drv[3] = {dr.x, dr.y, dr.z};
+            const T ulv[3] = {ul.x, ul.y, ul.z};
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) Ia.B.m[3 * r + c] = fmadd(-drv[r], ulv[c], IA.B.m[3 * r + c]);
+            Ia.M = S3<T>{fmadd(-dl.x, ul.x, IA.M.xx), fmadd(-dl.x, ul.y, IA.M.xy), fmadd(-dl.x, ul.z, IA.M.xz),
+                         fmadd(-dl.y, ul.y, IA.M.yy), fmadd(-dl.y, ul.z, IA.M.yz), fmadd(-dl.z, ul.z, IA.M.zz)};
+            // pa = pA + Ia c + U u / D,   c = (cw0, cw1, 0; cv0, cv1, 0)
+            const T a0 = cw0[j], a1 = cw1[j], b0 = cv0[j], b1 = cv1[j];
+            V3<T> pa_n = v3(fmadd(Ia.A.xx, a0, fmadd(Ia.A.xy, a1, fmadd(Ia.B.m[0], b0, fmadd(Ia.B.m[1], b1, fmadd(dr.x, u, pAn.x))))),
+                            fmadd(Ia.A.xy, a0, fmadd(Ia.A.yy, a1, fmadd(Ia.B.m[3], b0, fmadd(Ia.B.m[4], b1, fmadd(dr.y, u, pAn.y))))),
+                            fmadd(Ia.A.xz, a0, fmadd(Ia.A.yz, a1, fmadd(Ia.B.m[6], b0, fmadd(Ia.B.m[7], b1, fmadd(dr.z, u, pAn.z))))));
+            V3<T> pa_f = v3(fmadd(Ia.B.m[0], a0, fmadd(Ia.B.m[3], a1, fmadd(Ia.M.xx, b0, fmadd(Ia.M.xy, b1, fmadd(dl.x, u, pAf.x))))),
+                            fmadd(Ia.B.m[1], a0, fmadd(Ia.B.m[4], a1, fmadd(Ia.M.xy, b0, fmadd(Ia.M.yy, b1, fmadd(dl.y, u, pAf.y))))),
+                            fmadd(Ia.B.m[2], a0, fmadd(Ia.B.m[5], a1, fmadd(Ia.M.xz, b0, fmadd(Ia.M.yz, b1, fmadd(dl.z, u, pAf.z))))));
+            // to the parent frame
+            const Link<T> L = load_link(mdl, j);
+            const M3<T> E = joint_rotation(L.Rp, cs[j], sn[j]);
+            const V3<T> fl = mul(E, pa_f);
+            const V3<T> nl = cross_add(mul(E, pa_n), L.p, fl);
+            pAf = v3(pf[j - 1].x + fl.x, pf[j - 1].y + fl.y, pf[j - 1].z + fl.z);
+            pAn = v3(pn[j - 1].x + nl.x, pn[j - 1].y + nl.y, pn[j - 1].z + nl.z);
+            IA = to_parent(E, L.p, Ia);
+            add_rigid(IA, load_link(mdl, j - 1));
+        }
+    }
+
+    // Pass 3: accelerations, root to leaf.
+    reload_fence();
+    V3<T> aw = v3(T(0), T(0), T(0)), av = v3(T(0), T(0), T(0));
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const Link<T> L = load_link(mdl, j);
+        const M3<T> E = joint_rotation(L.Rp, cs[j], sn[j]);
+        if (j == 0) {
+            const T g = T(kGravity);
+            aw = v3(T(0), T(0), T(0));
+            av = v3(g * E.m[6], g * E.m[7], g * E.m[8]);
+        } else {
+            const V3<T> ua = cross_sub(av, L.p, aw);
+            aw = mul_t(E, aw);
+            av = mul_t(E, ua);
+        }
+        aw.x += cw0[j]; aw.y += cw1[j];
+        av.x += cv0[j]; av.y += cv1[j];
+        const T dot = fmadd(Ur[j][0], aw.x, fmadd(Ur[j][1], aw.y, fmadd(Ur[j][2], aw.z,
+                      fmadd(Ul[j][0], av.x, fmadd(Ul[j][1], av.y, Ul[j][2] * av.z)))));
+        const T a = (uu[j] - dot) * invD[j];
+        aw.z += a;
+        out(j, a);
+    }
+}
+
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                         const T *__restrict__ tau, T *__restrict__ qdd, uint32_t b,
+                                         int64_t ld) {
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    T qv[N], qdv[N], tv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qv[j] = ld_row(q, j * ld, off);
+        qdv[j] = ld_row(qd, j * ld, off);
+        tv[j] = ld_row(tau, j * ld, off);
+    }
+    aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
+}
+
+}  // namespace dev
+}  // namespace rbamd

@@ -128,22 +128,38 @@ int device_consts(const Multibody *mb, const T **out) {
     return RB_OK;
 }
 
-// The hipRTC kernel for this model on the current device, or nullptr (generic path).
-const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast) {
+// The hipRTC kernel of `kind` for this model on the current device, or nullptr (the
+// precompiled generic kernel then runs).
+const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f64, bool fast) {
     if (!rbamd::jit_enabled()) return nullptr;
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
-    const bool stream = rbamd::rnea_use_stream(f64, mb->model.n, true);
+    const bool stream = kind == rbamd::JitKind::Rnea && rbamd::rnea_use_stream(f64, mb->model.n, true);
     const bool fst = fast && !f64;
-    const std::string key = std::to_string(d) + (f64 ? ":f64" : ":f32") + (fst ? ":fast" : ":precise") +
-                            (stream ? ":stream" : ":lane") + ":nt" + std::to_string(rbamd::tuning().rnea_nt & 3);
+    const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
+                            (fst ? ":fast" : ":precise") + (stream ? ":stream" : ":lane") + ":nt" +
+                            std::to_string(kind == rbamd::JitKind::Rnea ? (rbamd::tuning().rnea_nt & 3) : 0);
     std::lock_guard<std::mutex> lk(mb->mu);
     auto it = mb->jit.find(key);
     if (it == mb->jit.end()) {
-        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, rbamd::JitKind::Rnea, f64, fst, stream)).first;
+        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, stream)).first;
         mb->jit_device[key] = d;
     }
     return it->second.function ? &it->second : nullptr;
+}
+
+const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast) {
+    return jit_get(mb, rbamd::JitKind::Rnea, f64, fast);
+}
+
+hipError_t jit_launch(const rbamd::JitKernel *jk, hipFunction_t fn, uint32_t B, void **args, hipStream_t s) {
+    const unsigned full = (B + 255u) / 256u;
+    unsigned g = full;
+    if (jk->stream) {
+        const int f = rbamd::tuning().grid_factor < 1 ? 1 : rbamd::tuning().grid_factor;
+        g = jk->resident * (unsigned)f < full ? jk->resident * (unsigned)f : full;
+    }
+    return hipModuleLaunchKernel(fn, g, 1, 1, 256, 1, 1, 0, s, args, nullptr);
 }
 
 template <typename T>
@@ -151,21 +167,37 @@ hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const 
                            uint32_t B, int64_t ld, hipStream_t s) {
     if (B == 0) return hipSuccess;
     if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig())) {
-        const unsigned full = (B + 255u) / 256u;
-        unsigned g = full;
-        if (jk->stream) {
-            const int f = rbamd::tuning().grid_factor < 1 ? 1 : rbamd::tuning().grid_factor;
-            g = jk->resident * (unsigned)f < full ? jk->resident * (unsigned)f : full;
-        }
         void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&ld};
         hipFunction_t fn = jk->function;
         const auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
         if (jk->tile_function && rbamd::tuning().rnea_tile && a16(q) && a16(qd) && a16(qdd) && a16(tau) &&
             ((uint64_t)ld * sizeof(T)) % 16 == 0)
             fn = jk->tile_function;
-        return hipModuleLaunchKernel(fn, g, 1, 1, 256, 1, 1, 0, s, args, nullptr);
+        return jit_launch(jk, fn, B, args, s);
     }
     return rbamd::launch_rnea<T>(mb->model.n, mdl, q, qd, qdd, tau, B, ld, s, fast_trig());
+}
+
+template <typename T>
+hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *tau, T *qdd,
+                         uint32_t B, int64_t ld, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Fd, sizeof(T) == 8, fast_trig())) {
+        void *args[] = {(void *)&q, (void *)&qd, (void *)&tau, (void *)&qdd, (void *)&B, (void *)&ld};
+        return jit_launch(jk, jk->function, B, args, s);
+    }
+    return rbamd::launch_aba<T>(mb->model.n, mdl, q, qd, tau, qdd, B, ld, s, fast_trig());
+}
+
+template <typename T>
+hipError_t launch_crba_any(const Multibody *mb, const T *mdl, const T *q, T *H, uint32_t B, int64_t ld,
+                           hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Crba, sizeof(T) == 8, false)) {
+        void *args[] = {(void *)&q, (void *)&H, (void *)&B, (void *)&ld};
+        return jit_launch(jk, jk->function, B, args, s);
+    }
+    return rbamd::launch_crba<T>(mb->model.n, mdl, q, H, B, ld, s);
 }
 
 constexpr int64_t kChunk = int64_t(1) << 28;  // per-launch batch cap: b * sizeof(T) < 2^32
@@ -278,8 +310,7 @@ int fd_batch(const Multibody *mb, const T *q, const T *qd, const T *tau, T *qdd,
     const T *mdl = nullptr;
     if ((rc = device_consts<T>(mb, &mdl))) return rc;
     return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = rbamd::launch_aba<T>(mb->model.n, mdl, q + b0, qd + b0, tau + b0, qdd + b0, nb, ld,
-                                            (hipStream_t)stream, fast_trig());
+        hipError_t e = launch_fd_any<T>(mb, mdl, q + b0, qd + b0, tau + b0, qdd + b0, nb, ld, (hipStream_t)stream);
         return e == hipSuccess ? RB_OK : hip_err(e, "aba launch");
     });
 }
@@ -293,7 +324,7 @@ int crba_batch(const Multibody *mb, const T *q, T *H, int64_t batch, int64_t ld,
     const T *mdl = nullptr;
     if ((rc = device_consts<T>(mb, &mdl))) return rc;
     return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = rbamd::launch_crba<T>(mb->model.n, mdl, q + b0, H + b0, nb, ld, (hipStream_t)stream);
+        hipError_t e = launch_crba_any<T>(mb, mdl, q + b0, H + b0, nb, ld, (hipStream_t)stream);
         return e == hipSuccess ? RB_OK : hip_err(e, "crba launch");
     });
 }
@@ -423,7 +454,7 @@ double *multibody_crba(const Multibody *mb, const double *q) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
         if (rc) return rc;
-        hipError_t e = rbamd::launch_crba<double>((int)n, mdl, din, dout, 1, 1, s);
+        hipError_t e = launch_crba_any<double>(mb, mdl, din, dout, 1, 1, s);
         return e == hipSuccess ? RB_OK : hip_err(e, "crba launch");
     });
 }
@@ -510,10 +541,11 @@ int multibody_limits(const Multibody *mb, double *lower, double *upper, double *
 
 int multibody_supported_dofs(int *out, int cap) { return rbamd::supported_dofs(out, cap); }
 
-int multibody_rnea_kernel_path(const Multibody *mb, int f64) {
+int multibody_kernel_path(const Multibody *mb, int kind, int f64) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
+    if (kind < 0 || kind > 2) return -set_err(RB_ERR_ARG, "kind must be 0 (rnea), 1 (fd) or 2 (crba)");
     if (!rbamd::jit_enabled()) return 0;
-    if (jit_rnea(mb, f64 != 0, fast_trig())) return 1;
+    if (jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 ? false : fast_trig())) return 1;
     int d = 0;
     (void)hipGetDevice(&d);
     std::lock_guard<std::mutex> lk(mb->mu);
@@ -522,10 +554,14 @@ int multibody_rnea_kernel_path(const Multibody *mb, int f64) {
     return 0;
 }
 
-int multibody_jit_source(const Multibody *mb, int f64, char *buf, int64_t cap) {
+int multibody_rnea_kernel_path(const Multibody *mb, int f64) { return multibody_kernel_path(mb, 0, f64); }
+
+int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    const std::string src = rbamd::jit_source(mb->model, rbamd::JitKind::Rnea, f64 != 0, fast_trig() && !f64,
-                                              rbamd::rnea_use_stream(f64 != 0, mb->model.n, true));
+    if (kind < 0 || kind > 2) return -set_err(RB_ERR_ARG, "kind must be 0 (rnea), 1 (fd) or 2 (crba)");
+    const std::string src = rbamd::jit_source(mb->model, (rbamd::JitKind)kind, f64 != 0,
+                                              kind != 2 && fast_trig() && !f64,
+                                              kind == 0 && rbamd::rnea_use_stream(f64 != 0, mb->model.n, true));
     if (buf && cap > 0) {
         const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
         std::memcpy(buf, src.data(), n);
@@ -534,12 +570,14 @@ int multibody_jit_source(const Multibody *mb, int f64, char *buf, int64_t cap) {
     return (int)src.size();
 }
 
-int64_t multibody_jit_compile(const Multibody *mb, int f64, const char *arch) {
+int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char *arch) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
+    if (kind < 0 || kind > 2) return -set_err(RB_ERR_ARG, "kind must be 0 (rnea), 1 (fd) or 2 (crba)");
     std::vector<char> code;
     std::string err;
-    if (!rbamd::jit_compile(mb->model, rbamd::JitKind::Rnea, f64 != 0, fast_trig() && !f64,
-                            rbamd::rnea_use_stream(f64 != 0, mb->model.n, true), arch ? arch : "gfx950", &code, &err))
+    if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && fast_trig() && !f64,
+                            kind == 0 && rbamd::rnea_use_stream(f64 != 0, mb->model.n, true),
+                            arch ? arch : "gfx950", &code, &err))
         return -set_err(RB_ERR_HIP, err);
     return (int64_t)code.size();
 }

@@ -6,55 +6,30 @@
 
 #include "dofs.hpp"
 #include "kernels.hpp"
-#include "spatial.hip.hpp"
-#include "artinertia.hip.hpp"
+#include "crba_body.hip.hpp"
 
 namespace rbamd {
 namespace dev {
 
 // ------------------------------------------------------------------------------ CRBA
-// multibody.rs:155-174: composite inertia leaf->root; column i of H from F = Ic_i S
-// carried to the root.  Output matches the ABI: n x n column-major per configuration,
-// H[j + n*i] for j <= i, strictly-lower entries written as exact zeros.
 template <typename T, int N, bool FAST>
 __global__ __launch_bounds__(kBlock) void crba_kernel(const T *__restrict__ gmdl,
                                                       const T *__restrict__ q,
                                                       T *__restrict__ H, uint32_t B,
                                                       int64_t ld) {
     __shared__ T mdl[N * kLinkStride];
-    stage_model<T, N, kBlock>(gmdl, mdl);
+    ModelStage<T, N, kBlock> st;
+    st.fetch(gmdl);
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
-    if (b >= B) return;
     const uint32_t off = b * (uint32_t)sizeof(T);
-    T cs[N], sn[N];
+    T qv[N];
+    if (b < B) {
 #pragma unroll
-    for (int j = 0; j < N; ++j) sin_cos<FAST>(ld_row(q, j * ld, off), sn[j], cs[j]);
-
-    ArtI<T> Ic = rigid_inertia(load_link(mdl, N - 1));
-#pragma unroll
-    for (int i = N - 1; i >= 0; --i) {
-        reload_fence();
-        st_row(H, (i + N * i) * ld, off, Ic.A.zz);  // get_rotz, inertia.rs:91-93
-#pragma unroll
-        for (int r = i + 1; r < N; ++r) st_row(H, (r + N * i) * ld, off, T(0));
-        V3<T> Fn = v3(Ic.A.xz, Ic.A.yz, Ic.A.zz);
-        V3<T> Ff = v3(Ic.B.m[6], Ic.B.m[7], Ic.B.m[8]);
-#pragma unroll
-        for (int j = i - 1; j >= 0; --j) {
-            const Link<T> L = load_link(mdl, j + 1);
-            const M3<T> E = joint_rotation(L.Rp, cs[j + 1], sn[j + 1]);
-            const V3<T> fl = mul(E, Ff);
-            Fn = cross_add(mul(E, Fn), L.p, fl);
-            Ff = fl;
-            st_row(H, (j + N * i) * ld, off, Fn.z);
-        }
-        if (i > 0) {
-            const Link<T> L = load_link(mdl, i);
-            const M3<T> E = joint_rotation(L.Rp, cs[i], sn[i]);
-            Ic = to_parent(E, L.p, Ic);
-            add_rigid(Ic, load_link(mdl, i - 1));
-        }
+        for (int j = 0; j < N; ++j) qv[j] = ld_row(q, j * ld, off);
     }
+    st.commit(mdl);
+    if (b >= B) return;
+    crba_eval<T, N, FAST>(mdl, qv, [&](int e, T v) { st_row(H, e * ld, off, v); });
 }
 
 }  // namespace dev

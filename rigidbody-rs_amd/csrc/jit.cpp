@@ -44,46 +44,61 @@ std::string literal(double x, bool f64) {
 }  // namespace
 
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream) {
-    (void)kind;
     std::vector<double> pk = m.pack_f64();
     for (int i = 0; i < m.n; ++i) {
         double *c = &pk[(size_t)i * kLinkStride];
         for (int k = 0; k < 9; ++k) c[kE0 + k] = snap(c[kE0 + k]);
         for (int k = 0; k < 3; ++k) c[kP + k] = snap(c[kP + k]);
     }
+    const char *F = fast ? "true" : "false";
     std::ostringstream o;
-    o << "#define RB_NT " << (tuning().rnea_nt & 3) << "\n";
-    o << "#include \"rnea_body.hip.hpp\"\n";
+    o << "#define RB_NT " << (kind == JitKind::Rnea ? (tuning().rnea_nt & 3) : 0) << "\n";
+    o << (kind == JitKind::Rnea ? "#include \"rnea_body.hip.hpp\"\n"
+          : kind == JitKind::Fd ? "#include \"aba_body.hip.hpp\"\n"
+                                : "#include \"crba_body.hip.hpp\"\n");
     o << "using T = " << (f64 ? "double" : "float") << ";\n";
     o << "constexpr int N = " << m.n << ";\n";
     o << "static __device__ constexpr T kModel[" << pk.size() << "] = {\n";
     for (size_t k = 0; k < pk.size(); ++k) o << "  " << literal(pk[k], f64) << ",\n";
     o << "};\n";
-    o << "extern \"C\" __global__ __launch_bounds__(256) void rb_jit_kernel(const T *__restrict__ q, "
-         "const T *__restrict__ qd, const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
-    o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
-    o << "  if (b >= B) return;\n";
-    const char *F = fast ? "true" : "false";
-    if (stream) {
-        o << "  T qv[N], qdv[N], qddv[N];\n";
-        o << "  rbamd::dev::load_cfg<T, N>(q, qd, qdd, ld, b * (uint32_t)sizeof(T), qv, qdv, qddv);\n";
-        o << "  rbamd::dev::rnea_stream_lane<T, N, " << F
-          << ">(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
+    const char *head = "extern \"C\" __global__ __launch_bounds__(256) void ";
+    if (kind == JitKind::Rnea) {
+        o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+             "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        if (stream) {
+            o << "  T qv[N], qdv[N], qddv[N];\n";
+            o << "  rbamd::dev::load_cfg<T, N>(q, qd, qdd, ld, b * (uint32_t)sizeof(T), qv, qdv, qddv);\n";
+            o << "  rbamd::dev::rnea_stream_lane<T, N, " << F
+              << ">(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
+        } else {
+            o << "  rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
+        }
+        o << "}\n";
+        if (jit_tile_ok(m.n, f64)) {
+            o << head << "rb_jit_tile(const T *__restrict__ q, const T *__restrict__ qd, "
+                 "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
+            o << "  __shared__ T tile[3 * N * 256];\n";
+            o << "  const uint32_t b0 = blockIdx.x * 256u;\n";
+            o << "  if (b0 + 256u <= B) {\n";
+            o << "    rbamd::dev::rnea_tile<T, N, " << F << ">(kModel, q, qd, qdd, tau, b0, ld, tile);\n";
+            o << "  } else {\n";
+            o << "    const uint32_t b = b0 + threadIdx.x;\n";
+            o << "    if (b < B) rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
+            o << "  }\n}\n";
+        }
+    } else if (kind == JitKind::Fd) {
+        o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+             "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld) {\n";
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        o << "  rbamd::dev::aba_lane<T, N, " << F << ">(kModel, q, qd, tau, qdd, b, ld);\n}\n";
     } else {
-        o << "  rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
-    }
-    o << "}\n";
-    if (jit_tile_ok(m.n, f64)) {
-        o << "extern \"C\" __global__ __launch_bounds__(256) void rb_jit_tile(const T *__restrict__ q, "
-             "const T *__restrict__ qd, const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
-        o << "  __shared__ T tile[3 * N * 256];\n";
-        o << "  const uint32_t b0 = blockIdx.x * 256u;\n";
-        o << "  if (b0 + 256u <= B) {\n";
-        o << "    rbamd::dev::rnea_tile<T, N, " << F << ">(kModel, q, qd, qdd, tau, b0, ld, tile);\n";
-        o << "  } else {\n";
-        o << "    const uint32_t b = b0 + threadIdx.x;\n";
-        o << "    if (b < B) rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
-        o << "  }\n}\n";
+        o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ H, uint32_t B, int64_t ld) {\n";
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        o << "  rbamd::dev::crba_lane<T, N, " << F << ">(kModel, q, H, b, ld);\n}\n";
     }
     return o.str();
 }
@@ -134,7 +149,8 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stre
         jk.module = nullptr;
         return jk;
     }
-    if (jit_tile_ok(m.n, f64) && hipModuleGetFunction(&jk.tile_function, jk.module, "rb_jit_tile") != hipSuccess)
+    if (kind == JitKind::Rnea && jit_tile_ok(m.n, f64) &&
+        hipModuleGetFunction(&jk.tile_function, jk.module, "rb_jit_tile") != hipSuccess)
         jk.tile_function = nullptr;
     e = hipModuleGetFunction(&jk.function, jk.module, "rb_jit_kernel");
     if (e != hipSuccess) {

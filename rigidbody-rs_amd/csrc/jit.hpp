@@ -23,7 +23,7 @@
 
 namespace rbamd {
 
-enum class JitKind : int { Rnea = 0 };
+enum class JitKind : int { Rnea = 0, Fd = 1, Crba = 2 };
 
 struct JitKernel {
     hipModule_t module = nullptr;

@@ -78,8 +78,10 @@ _sig("multibody_fwd_kin_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _v
 _sig("multibody_jac_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_rnea_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
 _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
-_sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, _i64])
-_sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_char_p])
+_sig("multibody_kernel_path", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int])
+_sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _i64])
+_sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
+KINDS = {"rnea": 0, "fd": 1, "crba": 2}
 _sig("rb_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
 _sig("rb_probe_rows_f32", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _i64, _i64, ctypes.c_int, _vp])
 _sig("multibody_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
@@ -234,21 +236,24 @@ class Multibody:
     def upload(self):
         _check(_lib.multibody_upload(self._h), "upload")
 
-    def rnea_kernel_path(self, f64=False) -> str:
-        """'jit' if the model-specialised hipRTC kernel runs on this device, else 'generic'."""
-        r = _lib.multibody_rnea_kernel_path(self._h, int(bool(f64)))
+    def kernel_path(self, kind="rnea", f64=False) -> str:
+        """'jit' if the model-specialised hipRTC kernel of `kind` runs on this device."""
+        r = _lib.multibody_kernel_path(self._h, KINDS[kind], int(bool(f64)))
         if r < 0:
             raise RigidBodyError(last_error())
         return "jit" if r == 1 else "generic"
 
-    def jit_source(self, f64=False) -> str:
-        n = _lib.multibody_jit_source(self._h, int(bool(f64)), None, 0)
+    def rnea_kernel_path(self, f64=False) -> str:
+        return self.kernel_path("rnea", f64)
+
+    def jit_source(self, f64=False, kind="rnea") -> str:
+        n = _lib.multibody_jit_source(self._h, KINDS[kind], int(bool(f64)), None, 0)
         buf = ctypes.create_string_buffer(n + 1)
-        _lib.multibody_jit_source(self._h, int(bool(f64)), buf, n + 1)
+        _lib.multibody_jit_source(self._h, KINDS[kind], int(bool(f64)), buf, n + 1)
         return buf.value.decode()
 
-    def jit_compile(self, f64=False, arch="gfx950") -> int:
-        r = _lib.multibody_jit_compile(self._h, int(bool(f64)), arch.encode())
+    def jit_compile(self, f64=False, arch="gfx950", kind="rnea") -> int:
+        r = _lib.multibody_jit_compile(self._h, KINDS[kind], int(bool(f64)), arch.encode())
         if r < 0:
             raise RigidBodyError(last_error())
         return r

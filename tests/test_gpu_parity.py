@@ -240,13 +240,19 @@ def test_jit_and_generic_kernels_agree(name, ffi, dev, fr3_text):
         for jit, tile in ((1, 1), (1, 0), (0, 1)):
             ffi.set_tuning("jit", jit)
             ffi.set_tuning("rnea_tile", tile)
-            assert mb.rnea_kernel_path(f64=False) == ("jit" if jit else "generic"), ffi.last_error()
-            assert mb.rnea_kernel_path(f64=True) == ("jit" if jit else "generic"), ffi.last_error()
+            for kind in ("rnea", "fd", "crba"):
+                for f64 in (False, True):
+                    assert mb.kernel_path(kind, f64) == ("jit" if jit else "generic"), ffi.last_error()
             q, qd, qdd = (_t(g[k], dev) for k in ("q", "qd", "qdd"))
             _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), g["tau"], 1e-9, f"rnea f64 jit={jit} tile={tile}")
             q32, qd32, qdd32 = (x.float() for x in (q, qd, qdd))
             ref = om.rnea_batch(*[x.double().cpu().numpy() for x in (q32, qd32, qdd32)])
             _close(mb.rnea_batch(q32, qd32, qdd32).cpu().numpy(), ref, 1e-4, f"rnea f32 jit={jit} tile={tile}")
+            tin = _t(g["tau_in"], dev)
+            qdd_gpu = mb.fd_batch(q, qd, tin).cpu().numpy()
+            res = om.rnea_batch(g["q"], g["qd"], qdd_gpu) - g["tau_in"]
+            assert (np.abs(res) / (1 + np.abs(g["tau_in"]))).max() <= 1e-8, f"fd f64 jit={jit}"
+            _close(mb.crba_batch(q).cpu().numpy(), g["H"], 1e-9, f"crba f64 jit={jit}")
     finally:
         ffi.set_tuning("jit", 1)
         ffi.set_tuning("rnea_tile", 1)
