@@ -10,6 +10,8 @@
  *                                 qdd = sym(H)^-1 (tau - rnea(q,qd,0)) with H from
  *                                 multibody_crba (multibody.rs:155-174), computed by the
  *                                 Articulated-Body Algorithm
+ *   multibody_rollout_batch_*  <- K fused forward-dynamics + semi-implicit Euler steps
+ *                                 (MPC shooting)
  *   multibody_crba_batch_*     <- multibody_crba      (lib.rs:32-43)
  *   multibody_fwd_kin_batch_*  <- multibody_fwd_kin   (lib.rs:46-57)
  *   multibody_jac_batch_*      <- multibody_jac       (lib.rs:60-70)
@@ -77,7 +79,7 @@ int multibody_supported_dofs(int *out, int cap);
 int multibody_upload(const Multibody *mb);
 
 /* Which kernel runs for this model on the current device; kind 0 = rnea, 1 = fd,
- * 2 = crba.  1 = model-specialised kernel compiled at first use by hipRTC, 0 =
+ * 2 = crba, 3 = rollout.  1 = model-specialised kernel compiled at first use by hipRTC, 0 =
  * precompiled generic kernel (also when hipRTC failed; rb_last_error() holds the log). */
 int multibody_kernel_path(const Multibody *mb, int kind, int f64);
 int multibody_rnea_kernel_path(const Multibody *mb, int f64);
@@ -114,6 +116,17 @@ int multibody_fd_batch_f32(const Multibody *mb, const float *q, const float *qd,
 int multibody_fd_batch_f64(const Multibody *mb, const double *q, const double *qd,
                            const double *tau, double *qdd, int64_t batch, int64_t ld,
                            void *stream);
+/* Fused rollout for MPC shooting: K steps of semi-implicit Euler on the forward dynamics
+ * above, qd += dt * qdd(q, qd, tau_k); q += dt * qd, state kept in registers.  q and qd
+ * ([n][ld]) are read and overwritten with the final state; tau_seq is [K][n][ld] (step k,
+ * joint j, config b at (k*n + j)*ld + b); traj (same shape, may be NULL) receives q after
+ * every step. */
+int multibody_rollout_batch_f32(const Multibody *mb, float *q, float *qd, const float *tau_seq,
+                                double dt, int K, float *traj, int64_t batch, int64_t ld,
+                                void *stream);
+int multibody_rollout_batch_f64(const Multibody *mb, double *q, double *qd, const double *tau_seq,
+                                double dt, int K, double *traj, int64_t batch, int64_t ld,
+                                void *stream);
 int multibody_crba_batch_f32(const Multibody *mb, const float *q, float *H,
                              int64_t batch, int64_t ld, void *stream);
 int multibody_crba_batch_f64(const Multibody *mb, const double *q, double *H,

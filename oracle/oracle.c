@@ -514,6 +514,23 @@ int oracle_fd(const oracle_model *m, const double *q, const double *qd,
     return 0;
 }
 
+/* Fused rollout: semi-implicit Euler on oracle_fd. */
+int oracle_rollout(const oracle_model *m, double *q, double *qd, const double *tau_seq,
+                   double dt, int K, double *traj) {
+    int n = m->n;
+    double qdd[ORACLE_MAX_DOF];
+    for (int k = 0; k < K; ++k) {
+        if (oracle_fd(m, q, qd, tau_seq + (long)k * n, qdd) != 0) return -1;
+        for (int j = 0; j < n; ++j) {
+            qd[j] += dt * qdd[j];
+            q[j] += dt * qd[j];
+        }
+        if (traj)
+            for (int j = 0; j < n; ++j) traj[(long)k * n + j] = q[j];
+    }
+    return 0;
+}
+
 /* ---------------------------------------------------------- batch drivers -- */
 static int pick_threads(int nthreads) {
 #ifdef _OPENMP
@@ -568,5 +585,29 @@ void oracle_crba_batch(const oracle_model *m, const double *q, double *H,
         for (int j = 0; j < n; ++j) x[j] = q[j * ld + b];
         oracle_crba(m, x, h);
         for (int e = 0; e < n * n; ++e) H[e * ld + b] = h[e];
+    }
+}
+
+void oracle_rollout_batch(const oracle_model *m, double *q, double *qd, const double *tau_seq,
+                          double dt, int K, double *traj, long batch, long ld, int nthreads) {
+    int n = m->n;
+    int nt = pick_threads(nthreads);
+    (void)nt;
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (long b = 0; b < batch; ++b) {
+        double x[ORACLE_MAX_DOF], y[ORACLE_MAX_DOF];
+        double t[64 * ORACLE_MAX_DOF], tr[64 * ORACLE_MAX_DOF];
+        for (int j = 0; j < n; ++j) { x[j] = q[j * ld + b]; y[j] = qd[j * ld + b]; }
+        for (int k0 = 0; k0 < K; k0 += 64) {
+            int kk = K - k0 < 64 ? K - k0 : 64;
+            for (int k = 0; k < kk; ++k)
+                for (int j = 0; j < n; ++j) t[k * n + j] = tau_seq[((long)(k0 + k) * n + j) * ld + b];
+            if (oracle_rollout(m, x, y, t, dt, kk, tr) != 0)
+                for (int j = 0; j < n; ++j) { x[j] = NAN; y[j] = NAN; }
+            if (traj)
+                for (int k = 0; k < kk; ++k)
+                    for (int j = 0; j < n; ++j) traj[((long)(k0 + k) * n + j) * ld + b] = tr[k * n + j];
+        }
+        for (int j = 0; j < n; ++j) { q[j * ld + b] = x[j]; qd[j * ld + b] = y[j]; }
     }
 }

@@ -59,6 +59,16 @@ void oracle_jac(const oracle_model *m, const double *q, double *J);     /* 95-10
 int oracle_fd(const oracle_model *m, const double *q, const double *qd,
               const double *tau, double *qdd);
 
+/* Fused rollout: K steps of semi-implicit Euler on the forward
+ * dynamics definition: qd += dt * fd(q, qd, tau_k); q += dt * qd.  tau_seq is K x n
+ * (step-major); q, qd are updated in place; traj (K x n, may be NULL) receives q after
+ * each step.  Returns 0, or -1 if an H is not SPD. */
+int oracle_rollout(const oracle_model *m, double *q, double *qd, const double *tau_seq,
+                   double dt, int K, double *traj);
+/* SoA batched rollout: q/qd [n][ld], tau_seq [K][n][ld], traj [K][n][ld] or NULL. */
+void oracle_rollout_batch(const oracle_model *m, double *q, double *qd, const double *tau_seq,
+                          double dt, int K, double *traj, long batch, long ld, int nthreads);
+
 /* Batched SoA drivers (x[j*ld + b]) over `nthreads` OpenMP threads (<=0: all). */
 void oracle_rnea_batch(const oracle_model *m, const double *q, const double *qd,
                        const double *qdd, double *tau, long batch, long ld, int nthreads);

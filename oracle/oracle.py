@@ -46,6 +46,8 @@ def lib():
         L.oracle_rnea_batch.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp, ctypes.c_long, ctypes.c_long, ctypes.c_int]
         L.oracle_fd_batch.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp, ctypes.c_long, ctypes.c_long, ctypes.c_int]
         L.oracle_crba_batch.argtypes = [ctypes.c_void_p, _dp, _dp, ctypes.c_long, ctypes.c_long, ctypes.c_int]
+        L.oracle_rollout_batch.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, ctypes.c_double, ctypes.c_int, _dp,
+                                           ctypes.c_long, ctypes.c_long, ctypes.c_int]
         L.oracle_quat_from_scaled_axis.argtypes = [_dp, _dp]
         L.oracle_quat_from_axis_angle.argtypes = [_dp, ctypes.c_double, _dp]
         L.oracle_quat_to_matrix.argtypes = [_dp, _dp]
@@ -141,6 +143,16 @@ class Model:
         qdd = np.empty_like(q)
         lib().oracle_fd_batch(self.ptr, _p(q), _p(qd), _p(tau), _p(qdd), B, B, int(nthreads))
         return qdd
+
+    def rollout_batch(self, q, qd, tau_seq, dt, want_traj=False, nthreads=0):
+        """K semi-implicit Euler steps; q, qd [n, B]; tau_seq [K, n, B].  Returns
+        (q_K, qd_K, traj [K, n, B] or None)."""
+        q, qd, tau_seq = _c(q).copy(), _c(qd).copy(), _c(tau_seq)
+        K, n, B = tau_seq.shape
+        traj = np.empty((K, n, B)) if want_traj else None
+        lib().oracle_rollout_batch(self.ptr, _p(q), _p(qd), _p(tau_seq), float(dt), int(K),
+                                   _p(traj) if traj is not None else None, B, B, int(nthreads))
+        return q, qd, traj
 
     def crba_batch(self, q, nthreads=0):
         q = _c(q)

@@ -38,6 +38,33 @@ __global__ __launch_bounds__(kBlock) void aba_kernel(const T *__restrict__ gmdl,
     aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
 }
 
+template <typename T, int N, bool FAST>
+__global__ __launch_bounds__(kBlock) void rollout_kernel(const T *__restrict__ gmdl, T *__restrict__ q,
+                                                         T *__restrict__ qd, const T *__restrict__ tau_seq, T dt,
+                                                         int K, T *__restrict__ traj, uint32_t B, int64_t ld) {
+    __shared__ T mdl[N * kLinkStride];
+    ModelStage<T, N, kBlock> st;
+    st.fetch(gmdl);
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    T qv[N], qdv[N];
+    if (b < B) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q, j * ld, off);
+            qdv[j] = ld_row(qd, j * ld, off);
+        }
+    }
+    st.commit(mdl);
+    if (b >= B) return;
+    rollout_eval<T, N, FAST>(mdl, qv, qdv, tau_seq, dt, K, traj, ld, off);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        st_row(q, j * ld, off, qv[j]);
+        st_row(qd, j * ld, off, qdv[j]);
+    }
+}
+
 }  // namespace dev
 
 template <typename T>
@@ -65,6 +92,36 @@ hipError_t launch_aba(int n, const T *mdl, const T *q, const T *qd, const T *tau
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_rollout(int n, const T *mdl, T *q, T *qd, const T *tau_seq, T dt, int K, T *traj, uint32_t B,
+                          int64_t ld, hipStream_t s, bool fast) {
+    if (B == 0) return hipSuccess;
+    const dim3 grid(dev::grid_for(B)), block(dev::kBlock);
+    switch (n) {
+#define RB_CASE(N)                                                                                        \
+    case N:                                                                                               \
+        if constexpr (sizeof(T) == 4) {                                                                    \
+            if (fast) {                                                                                    \
+                hipLaunchKernelGGL((dev::rollout_kernel<T, N, true>), grid, block, 0, s, mdl, q, qd, tau_seq, \
+                                   dt, K, traj, B, ld);                                                    \
+                break;                                                                                     \
+            }                                                                                              \
+        }                                                                                                  \
+        hipLaunchKernelGGL((dev::rollout_kernel<T, N, false>), grid, block, 0, s, mdl, q, qd, tau_seq, dt, K,  \
+                           traj, B, ld);                                                                   \
+        break;
+        RB_FOR_EACH_DOF(RB_CASE)
+#undef RB_CASE
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template hipError_t launch_rollout<float>(int, const float *, float *, float *, const float *, float, int, float *,
+                                          uint32_t, int64_t, hipStream_t, bool);
+template hipError_t launch_rollout<double>(int, const double *, double *, double *, const double *, double, int,
+                                           double *, uint32_t, int64_t, hipStream_t, bool);
 template hipError_t launch_aba<float>(int, const float *, const float *, const float *, const float *, float *, uint32_t, int64_t, hipStream_t, bool);
 template hipError_t launch_aba<double>(int, const double *, const double *, const double *, const double *, double *, uint32_t, int64_t, hipStream_t, bool);
 

@@ -134,5 +134,49 @@ __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, 
     aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
 }
 
+// Fused rollout (the MPC-shooting use of forward dynamics): K steps
+// of semi-implicit Euler, qd += dt * fd(q, qd, tau_k); q += dt * qd, with the state kept
+// in registers across steps.  q, qd [n][ld] are read once and overwritten with the final
+// state; tau_seq is [K][n][ld]; traj ([K][n][ld], optional) receives q after each step.
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void rollout_eval(const T *mdl, T (&qv)[N], T (&qdv)[N],
+                                             const T *__restrict__ tau_seq, T dt, int K,
+                                             T *__restrict__ traj, int64_t ld, uint32_t off) {
+    for (int k = 0; k < K; ++k) {
+        T tv[N], a[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
+        aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { a[j] = v; });
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qdv[j] = fmadd(dt, a[j], qdv[j]);
+            qv[j] = fmadd(dt, qdv[j], qv[j]);
+        }
+        if (traj) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) st_row(traj, ((int64_t)k * N + j) * ld, off, qv[j]);
+        }
+    }
+}
+
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T *__restrict__ qd,
+                                             const T *__restrict__ tau_seq, T dt, int K, T *__restrict__ traj,
+                                             uint32_t b, int64_t ld) {
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    T qv[N], qdv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qv[j] = ld_row(q, j * ld, off);
+        qdv[j] = ld_row(qd, j * ld, off);
+    }
+    rollout_eval<T, N, FAST>(mdl, qv, qdv, tau_seq, dt, K, traj, ld, off);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        st_row(q, j * ld, off, qv[j]);
+        st_row(qd, j * ld, off, qdv[j]);
+    }
+}
+
 }  // namespace dev
 }  // namespace rbamd

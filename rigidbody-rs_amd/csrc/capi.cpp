@@ -190,6 +190,18 @@ hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T 
 }
 
 template <typename T>
+hipError_t launch_rollout_any(const Multibody *mb, const T *mdl, T *q, T *qd, const T *tau_seq, T dt, int K, T *traj,
+                              uint32_t B, int64_t ld, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Rollout, sizeof(T) == 8, fast_trig())) {
+        void *args[] = {(void *)&q, (void *)&qd, (void *)&tau_seq, (void *)&dt, (void *)&K, (void *)&traj,
+                        (void *)&B, (void *)&ld};
+        return jit_launch(jk, jk->function, B, args, s);
+    }
+    return rbamd::launch_rollout<T>(mb->model.n, mdl, q, qd, tau_seq, dt, K, traj, B, ld, s, fast_trig());
+}
+
+template <typename T>
 hipError_t launch_crba_any(const Multibody *mb, const T *mdl, const T *q, T *H, uint32_t B, int64_t ld,
                            hipStream_t s) {
     if (B == 0) return hipSuccess;
@@ -312,6 +324,23 @@ int fd_batch(const Multibody *mb, const T *q, const T *qd, const T *tau, T *qdd,
     return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
         hipError_t e = launch_fd_any<T>(mb, mdl, q + b0, qd + b0, tau + b0, qdd + b0, nb, ld, (hipStream_t)stream);
         return e == hipSuccess ? RB_OK : hip_err(e, "aba launch");
+    });
+}
+
+template <typename T>
+int rollout_batch(const Multibody *mb, T *q, T *qd, const T *tau_seq, double dt, int K, T *traj, int64_t batch,
+                  int64_t ld, void *stream) {
+    int rc = check_batch(mb, batch, ld);
+    if (rc) return rc;
+    if (K < 0) return set_err(RB_ERR_ARG, "negative step count");
+    if (batch == 0 || K == 0) return RB_OK;
+    if (!q || !qd || !tau_seq) return set_err(RB_ERR_NULL, "NULL array");
+    const T *mdl = nullptr;
+    if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
+        hipError_t e = launch_rollout_any<T>(mb, mdl, q + b0, qd + b0, tau_seq + b0, (T)dt, K,
+                                             traj ? traj + b0 : nullptr, nb, ld, (hipStream_t)stream);
+        return e == hipSuccess ? RB_OK : hip_err(e, "rollout launch");
     });
 }
 
@@ -543,7 +572,7 @@ int multibody_supported_dofs(int *out, int cap) { return rbamd::supported_dofs(o
 
 int multibody_kernel_path(const Multibody *mb, int kind, int f64) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 2) return -set_err(RB_ERR_ARG, "kind must be 0 (rnea), 1 (fd) or 2 (crba)");
+    if (kind < 0 || kind > 3) return -set_err(RB_ERR_ARG, "kind must be 0 rnea, 1 fd, 2 crba or 3 rollout");
     if (!rbamd::jit_enabled()) return 0;
     if (jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 ? false : fast_trig())) return 1;
     int d = 0;
@@ -558,7 +587,7 @@ int multibody_rnea_kernel_path(const Multibody *mb, int f64) { return multibody_
 
 int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 2) return -set_err(RB_ERR_ARG, "kind must be 0 (rnea), 1 (fd) or 2 (crba)");
+    if (kind < 0 || kind > 3) return -set_err(RB_ERR_ARG, "kind must be 0 rnea, 1 fd, 2 crba or 3 rollout");
     const std::string src = rbamd::jit_source(mb->model, (rbamd::JitKind)kind, f64 != 0,
                                               kind != 2 && fast_trig() && !f64,
                                               kind == 0 && rbamd::rnea_use_stream(f64 != 0, mb->model.n, true));
@@ -572,7 +601,7 @@ int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int6
 
 int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char *arch) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 2) return -set_err(RB_ERR_ARG, "kind must be 0 (rnea), 1 (fd) or 2 (crba)");
+    if (kind < 0 || kind > 3) return -set_err(RB_ERR_ARG, "kind must be 0 rnea, 1 fd, 2 crba or 3 rollout");
     std::vector<char> code;
     std::string err;
     if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && fast_trig() && !f64,
@@ -633,6 +662,14 @@ int multibody_fd_batch_f32(const Multibody *mb, const float *q, const float *qd,
 int multibody_fd_batch_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
                            double *qdd, int64_t batch, int64_t ld, void *stream) {
     return fd_batch<double>(mb, q, qd, tau, qdd, batch, ld, stream);
+}
+int multibody_rollout_batch_f32(const Multibody *mb, float *q, float *qd, const float *tau_seq, double dt, int K,
+                                 float *traj, int64_t batch, int64_t ld, void *stream) {
+    return rollout_batch<float>(mb, q, qd, tau_seq, dt, K, traj, batch, ld, stream);
+}
+int multibody_rollout_batch_f64(const Multibody *mb, double *q, double *qd, const double *tau_seq, double dt, int K,
+                                 double *traj, int64_t batch, int64_t ld, void *stream) {
+    return rollout_batch<double>(mb, q, qd, tau_seq, dt, K, traj, batch, ld, stream);
 }
 int multibody_crba_batch_f32(const Multibody *mb, const float *q, float *H, int64_t batch, int64_t ld,
                              void *stream) {

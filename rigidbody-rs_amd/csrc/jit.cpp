@@ -53,9 +53,9 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     const char *F = fast ? "true" : "false";
     std::ostringstream o;
     o << "#define RB_NT " << (kind == JitKind::Rnea ? (tuning().rnea_nt & 3) : 0) << "\n";
-    o << (kind == JitKind::Rnea ? "#include \"rnea_body.hip.hpp\"\n"
-          : kind == JitKind::Fd ? "#include \"aba_body.hip.hpp\"\n"
-                                : "#include \"crba_body.hip.hpp\"\n");
+    o << (kind == JitKind::Rnea                               ? "#include \"rnea_body.hip.hpp\"\n"
+          : (kind == JitKind::Fd || kind == JitKind::Rollout) ? "#include \"aba_body.hip.hpp\"\n"
+                                                              : "#include \"crba_body.hip.hpp\"\n");
     o << "using T = " << (f64 ? "double" : "float") << ";\n";
     o << "constexpr int N = " << m.n << ";\n";
     o << "static __device__ constexpr T kModel[" << pk.size() << "] = {\n";
@@ -94,6 +94,12 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
         o << "  rbamd::dev::aba_lane<T, N, " << F << ">(kModel, q, qd, tau, qdd, b, ld);\n}\n";
+    } else if (kind == JitKind::Rollout) {
+        o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
+             "int K, T *__restrict__ traj, uint32_t B, int64_t ld) {\n";
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        o << "  rbamd::dev::rollout_lane<T, N, " << F << ">(kModel, q, qd, tau_seq, dt, K, traj, b, ld);\n}\n";
     } else {
         o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ H, uint32_t B, int64_t ld) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";

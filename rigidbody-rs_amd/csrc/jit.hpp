@@ -23,7 +23,7 @@
 
 namespace rbamd {
 
-enum class JitKind : int { Rnea = 0, Fd = 1, Crba = 2 };
+enum class JitKind : int { Rnea = 0, Fd = 1, Crba = 2, Rollout = 3 };
 
 struct JitKernel {
     hipModule_t module = nullptr;

@@ -33,6 +33,9 @@ template <typename T>
 hipError_t launch_aba(int n, const T *mdl, const T *q, const T *qd, const T *tau, T *qdd,
                       uint32_t B, int64_t ld, hipStream_t s, bool fast);
 template <typename T>
+hipError_t launch_rollout(int n, const T *mdl, T *q, T *qd, const T *tau_seq, T dt, int K, T *traj, uint32_t B,
+                          int64_t ld, hipStream_t s, bool fast);
+template <typename T>
 hipError_t launch_crba(int n, const T *mdl, const T *q, T *H, uint32_t B, int64_t ld,
                        hipStream_t s);
 template <typename T>

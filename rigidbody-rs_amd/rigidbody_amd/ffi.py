@@ -81,7 +81,10 @@ _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
 _sig("multibody_kernel_path", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int])
 _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
-KINDS = {"rnea": 0, "fd": 1, "crba": 2}
+KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3}
+for _t in ("f32", "f64"):
+    _sig(f"multibody_rollout_batch_{_t}", ctypes.c_int,
+         [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_int, _vp, _i64, _i64, _vp])
 _sig("rb_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
 _sig("rb_probe_rows_f32", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _i64, _i64, ctypes.c_int, _vp])
 _sig("multibody_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
@@ -311,6 +314,27 @@ class Multibody:
         _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), out.data_ptr(), B, ld,
                   _stream_ptr(stream)), "fd_batch")
         return out
+
+    def rollout_batch(self, q, qd, tau_seq, dt, traj=False, stream=None):
+        """K fused forward-dynamics + semi-implicit Euler steps, in place on q and qd
+        ([n, B] CUDA tensors); tau_seq [K, n, B].  Returns the trajectory [K, n, B] of q
+        when traj=True (else None)."""
+        q = _soa(q, self.n, "q")
+        B = q.shape[1]
+        qd = _soa(qd, self.n, "qd", q.dtype, B)
+        if not isinstance(tau_seq, torch.Tensor) or tau_seq.dim() != 3 or tau_seq.shape[1:] != (self.n, B):
+            raise ValueError(f"tau_seq must be [K, {self.n}, {B}]")
+        if tau_seq.dtype != q.dtype or not tau_seq.is_contiguous():
+            raise ValueError("tau_seq must be contiguous with the state's dtype")
+        ld = _same_ld((q, qd))
+        if B > 1 and ld != B:
+            raise ValueError("rollout needs contiguous [n, B] state (ld == B), like tau_seq")
+        K = tau_seq.shape[0]
+        tr = torch.empty_like(tau_seq) if traj else None
+        fn = getattr(_lib, f"multibody_rollout_batch_{_TORCH_SUFFIX[q.dtype]}")
+        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau_seq.data_ptr(), float(dt), int(K),
+                  tr.data_ptr() if tr is not None else None, B, max(ld, B, 1), _stream_ptr(stream)), "rollout_batch")
+        return tr
 
     def crba_batch(self, q, out=None, stream=None):
         q = _soa(q, self.n, "q")

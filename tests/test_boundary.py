@@ -204,7 +204,7 @@ def test_jit_source_and_compile(ffi, fr3_text):
     assert "constexpr int N = 7" in src and "rnea_lane" in src
     assert "0.333000004f" in src  # fr3_joint1 origin z (fr3.urdf:62) as an fp32 literal
     assert "2.22044605e-16" not in src  # rotation residues snapped to exact 0
-    for kind in ("rnea", "fd", "crba"):
+    for kind in ("rnea", "fd", "crba", "rollout"):
         for f64 in (False, True):
             assert mb.jit_compile(f64=f64, kind=kind) > 1000
     assert "aba_lane" in mb.jit_source(kind="fd") and "crba_lane" in mb.jit_source(kind="crba")

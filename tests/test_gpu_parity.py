@@ -303,3 +303,38 @@ def test_cpp_consumer_drop_in(tmp_path, dev):
     _close(lines["pos"], g["fwd_kin"], 1e-9, "consumer fwd_kin")
     _close(lines["jac"], g["jac_raw"], 1e-9, "consumer jac")
     _close(lines["crba"], g["crba_raw"], 1e-9, "consumer crba")
+
+
+# ------------------------------------------------------------ fused rollout
+@pytest.mark.parametrize("name", ["fr3_golden.npz", "chain12_golden.npz"])
+def test_rollout_vs_oracle(name, ffi, dev, fr3_text):
+    """K = 16 fused forward-dynamics + semi-implicit Euler steps
+    against the oracle's step-by-step rollout; fp64 to 1e-9, fp32 to 1e-4 (scaled)."""
+    g = load_npz(name)
+    xml = _model_xml(name, fr3_text)
+    mb = ffi.Multibody.from_urdf_string(xml)
+    om = _oracle(xml)
+    n, B = g["q"].shape
+    K, dt = 16, 1e-3
+    rng = np.random.default_rng(3)
+    tau_seq = g["tau_in"][None, :, :] * rng.uniform(0.5, 1.0, (K, 1, B))
+    q_ref, qd_ref, traj_ref = om.rollout_batch(g["q"], g["qd"], tau_seq, dt, want_traj=True)
+    for dtype, tol in ((torch.float64, 1e-9), (torch.float32, 1e-4)):
+        q = _t(g["q"], dev, dtype)
+        qd = _t(g["qd"], dev, dtype)
+        ts = torch.as_tensor(tau_seq, dtype=dtype, device=dev).contiguous()
+        traj = mb.rollout_batch(q, qd, ts, dt, traj=True)
+        if dtype == torch.float32:  # reference from the fp32-rounded inputs
+            qr, qdr, tr = om.rollout_batch(g["q"].astype(np.float32).astype(float),
+                                           g["qd"].astype(np.float32).astype(float),
+                                           tau_seq.astype(np.float32).astype(float), dt, want_traj=True)
+        else:
+            qr, qdr, tr = q_ref, qd_ref, traj_ref
+        _close(q.cpu().numpy(), qr, tol, f"rollout q {dtype}")
+        _close(qd.cpu().numpy(), qdr, tol * 10, f"rollout qd {dtype}")
+        _close(traj.cpu().numpy(), tr, tol, f"rollout traj {dtype}")
+    # no trajectory requested: same final state
+    q = _t(g["q"], dev)
+    qd = _t(g["qd"], dev)
+    assert mb.rollout_batch(q, qd, torch.as_tensor(tau_seq, device=dev), dt) is None
+    _close(q.cpu().numpy(), q_ref, 1e-9, "rollout q (no traj)")
