@@ -102,34 +102,26 @@ def make_sets(mb, B, dtype, kernel, nsets, seed):
     return sets
 
 
-def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1):
-    """Warmup, then exactly `steps` launches bracketed by barrier + synchronize and by one
-    hipEvent pair on the launch stream (no per-launch events inside the timed region:
-    an event record between launches on one stream inflates a ~22 us step to ~32 us).
-    With streams > 1 consecutive batches rotate over that many streams (independent
-    batches overlap the previous launch's ramp/tail); the event pair then spans all of
-    them.  Returns (wall s, device ms per launch)."""
-    lib = ffi.lib()
-    suffix = "f32" if dtype == torch.float32 else "f64"
-    fn = getattr(lib, f"multibody_{'rnea' if kernel == 'rnea' else 'fd'}_batch_{suffix}")
+def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1):
+    """launch(i, stream_ptr) issues step i.  Warmup, then exactly `steps` launches
+    bracketed by barrier + synchronize and one hipEvent pair on the launch stream (no
+    per-launch events inside the timed region: an event record between launches on one
+    stream inflates a ~22 us step to ~32 us).  With streams > 1 consecutive steps rotate
+    over that many streams (independent batches overlap the previous launch's ramp and
+    tail); the event pair then spans all of them.  Returns (wall s, device ms per step)."""
     main = torch.cuda.current_stream()
     strs = [main] + [torch.cuda.Stream() for _ in range(streams - 1)]
-    B = sets[0][1].shape[1]
-    args = [[(mb.handle, ins[0].data_ptr(), ins[1].data_ptr(), ins[2].data_ptr(), out.data_ptr(), B, B,
-              ctypes.c_void_p(st.cuda_stream)) for st in strs] for ins, out in sets]
-    ns = len(args)
+    sps = [ctypes.c_void_p(st.cuda_stream) for st in strs]
     # spin-up: the clock ramps over the first tens of ms of load (DESIGN.md §5)
     t_spin = time.perf_counter()
     i = 0
     while (time.perf_counter() - t_spin) * 1e3 < spinup_ms:
-        fn(*args[i % ns][i % streams])
+        launch(i, sps[i % streams])
         i += 1
         if i % 64 == 0:
             torch.cuda.synchronize()
     for i in range(warmup):
-        rc = fn(*args[i % ns][i % streams])
-        if rc:
-            raise RuntimeError(ffi.last_error())
+        launch(i, sps[i % streams])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ends = [torch.cuda.Event() for _ in strs]
     if world > 1:
@@ -140,9 +132,7 @@ def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, stre
     for st in strs[1:]:
         st.wait_event(e0)
     for i in range(steps):
-        rc = fn(*args[i % ns][i % streams])
-        if rc:
-            raise RuntimeError(ffi.last_error())
+        launch(i, sps[i % streams])
     for st, end in zip(strs[1:], ends[1:]):
         end.record(st)
         main.wait_event(end)
@@ -152,6 +142,75 @@ def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, stre
     if world > 1:
         torch.distributed.barrier()
     return t1 - t0, e0.elapsed_time(e1) / steps
+
+
+def batch_launcher(mb, sets, kernel, dtype):
+    """Closure issuing the rnea / fd batched entry point on input set i % len(sets)."""
+    lib = ffi.lib()
+    suffix = "f32" if dtype == torch.float32 else "f64"
+    fn = getattr(lib, f"multibody_{'rnea' if kernel == 'rnea' else 'fd'}_batch_{suffix}")
+    B = sets[0][1].shape[1]
+    args = [(mb.handle, ins[0].data_ptr(), ins[1].data_ptr(), ins[2].data_ptr(), out.data_ptr(), B, B)
+            for ins, out in sets]
+    ns = len(args)
+
+    def launch(i, sp):
+        rc = fn(*args[i % ns], sp)
+        if rc:
+            raise RuntimeError(ffi.last_error())
+
+    return launch
+
+
+def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1):
+    return time_launches(batch_launcher(mb, sets, kernel, dtype), steps, warmup, world, spinup_ms, streams)
+
+
+def side_workloads(mb7, a, rotate_gib):
+    """Secondary measurements (one GPU, serial launches): the other BASELINE configs."""
+    sec = {}
+    B = a.batch
+    steps = max(20, a.steps // 4)
+
+    def one(name, mb, kernel, dt_name, bytes_per_cfg):
+        ds = DT[dt_name]
+        per = 4 * mb.n * B * (4 if dt_name == "f32" else 8)
+        sets = make_sets(mb, B, ds, kernel, max(2, int(np.ceil(rotate_gib * (1 << 30) / per))), chains.SEED + 31)
+        w, km = run_timed(mb, sets, kernel, ds, steps, 5, 1, 100.0)
+        sec[name] = {"evals_per_s": B * steps / w, "kernel_ms_avg": km,
+                     "hbm_frac": bytes_per_cfg * B / (km * 1e-3) / HBM_PEAK,
+                     "kernel_path": mb.kernel_path(kernel, dt_name == "f64")}
+        del sets
+        torch.cuda.empty_cache()
+
+    one("rnea_fr3_f64", mb7, "rnea", "f64", 224)
+    one("fd_fr3_f32", mb7, "fd", "f32", 112)            # BASELINE config 3 (ABA fp32)
+    one("fd_fr3_f64", mb7, "fd", "f64", 224)            # config 4 is rnea_f64 + fd_f64
+    mb30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
+    mb30.upload()
+    one("rnea_chain30_f32", mb30, "rnea", "f32", 480)   # config 5
+    # fused rollout: K forward-dynamics + Euler steps per launch, fp32, FR3
+    K, dt = 16, 1e-3
+    q = torch.empty((7, B), dtype=torch.float32, device="cuda")
+    qd = torch.empty_like(q)
+    lim = mb7.limits()
+    ffi.fill_uniform(q, *chains.input_ranges(lim, "q"), chains.SEED)
+    ffi.fill_uniform(qd, *chains.input_ranges(lim, "qd"), chains.SEED + 1)
+    tau = torch.empty((K * 7, B), dtype=torch.float32, device="cuda")
+    lo, hi = chains.input_ranges(lim, "tau")
+    ffi.fill_uniform(tau, lo * K, hi * K, chains.SEED + 2)
+    fn = ffi.lib().multibody_rollout_batch_f32
+
+    def launch(i, sp):
+        rc = fn(mb7.handle, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), dt, K, None, B, B, sp)
+        if rc:
+            raise RuntimeError(ffi.last_error())
+
+    w, km = time_launches(launch, max(10, steps // 4), 3, 1, 100.0)
+    sec["rollout_fr3_f32_K16"] = {"steps_per_launch": K, "evals_per_s": B * K * max(10, steps // 4) / w,
+                                  "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", False),
+                                  "note": "evals = configurations x Euler steps; state stays in registers"}
+    return sec
 
 
 def cpu_baseline(n, B_sample_hint, kernel, cpu_seconds):
@@ -244,23 +303,14 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(n, a.batch, a.kernel, a.cpu_seconds)
-    if rank == 0 and not a.no_secondary and world == 1:
-        sec = {}
+    if rank == 0 and not a.no_secondary and world == 1 and n == 7:
         # the same workload with consecutive batches overlapped on 2 streams
         w2, k2 = run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0, 2)
-        sec[f"{a.kernel}_{a.dtype}_2streams"] = {"evals_per_s": a.batch * a.steps / w2, "step_ms_device": k2,
-                                                  "hbm_frac_effective": bytes_per_eval * a.batch / (k2 * 1e-3) / HBM_PEAK}
-        for kern, dt in (("rnea", "f64"), ("fd", "f32"), ("fd", "f64")):
-            ds = DT[dt]
-            es = 4 if dt == "f32" else 8
-            ps = 4 * n * a.batch * es
-            ns = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / ps)))
-            del sets
-            torch.cuda.empty_cache()
-            sets = make_sets(mb, a.batch, ds, kern, ns, chains.SEED + 31)
-            w, km = run_timed(mb, sets, kern, ds, max(20, a.steps // 4), 5, 1, 100.0)
-            sec[f"{kern}_{dt}"] = {"evals_per_s": a.batch * max(20, a.steps // 4) / w, "kernel_ms_avg": km,
-                                   "hbm_frac": 4 * n * es * a.batch / (km * 1e-3) / HBM_PEAK}
+        sec = {f"{a.kernel}_{a.dtype}_2streams": {"evals_per_s": a.batch * a.steps / w2, "step_ms_device": k2,
+                                                   "hbm_frac_effective": bytes_per_eval * a.batch / (k2 * 1e-3) / HBM_PEAK}}
+        del sets
+        torch.cuda.empty_cache()
+        sec.update(side_workloads(mb, a, a.rotate_gib))
         line["secondary"] = sec
     if rank == 0:
         print(json.dumps(line), flush=True)
