@@ -162,6 +162,30 @@ def batch_launcher(mb, sets, kernel, dtype):
     return launch
 
 
+def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED):
+    """Closure issuing multibody_rollout_batch_* on one resident state (q, qd updated in
+    place by every launch) and a [K*n, B] torque sequence."""
+    n = mb.n
+    q = torch.empty((n, B), dtype=dtype, device="cuda")
+    qd = torch.empty_like(q)
+    lim = mb.limits()
+    ffi.fill_uniform(q, *chains.input_ranges(lim, "q"), seed)
+    ffi.fill_uniform(qd, *chains.input_ranges(lim, "qd"), seed + 1)
+    tau = torch.empty((K * n, B), dtype=dtype, device="cuda")
+    lo, hi = chains.input_ranges(lim, "tau")
+    ffi.fill_uniform(tau, lo * K, hi * K, seed + 2)
+    fn = getattr(ffi.lib(), f"multibody_rollout_batch_{'f32' if dtype == torch.float32 else 'f64'}")
+    args = (mb.handle, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), dt, K, None, B, B)
+
+    def launch(i, sp):
+        rc = fn(*args, sp)
+        if rc:
+            raise RuntimeError(ffi.last_error())
+
+    launch.keep = (q, qd, tau)
+    return launch
+
+
 def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1):
     return time_launches(batch_launcher(mb, sets, kernel, dtype), steps, warmup, world, spinup_ms, streams)
 
@@ -190,22 +214,8 @@ def side_workloads(mb7, a, rotate_gib):
     mb30.upload()
     one("rnea_chain30_f32", mb30, "rnea", "f32", 480)   # config 5
     # fused rollout: K forward-dynamics + Euler steps per launch, fp32, FR3
-    K, dt = 16, 1e-3
-    q = torch.empty((7, B), dtype=torch.float32, device="cuda")
-    qd = torch.empty_like(q)
-    lim = mb7.limits()
-    ffi.fill_uniform(q, *chains.input_ranges(lim, "q"), chains.SEED)
-    ffi.fill_uniform(qd, *chains.input_ranges(lim, "qd"), chains.SEED + 1)
-    tau = torch.empty((K * 7, B), dtype=torch.float32, device="cuda")
-    lo, hi = chains.input_ranges(lim, "tau")
-    ffi.fill_uniform(tau, lo * K, hi * K, chains.SEED + 2)
-    fn = ffi.lib().multibody_rollout_batch_f32
-
-    def launch(i, sp):
-        rc = fn(mb7.handle, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), dt, K, None, B, B, sp)
-        if rc:
-            raise RuntimeError(ffi.last_error())
-
+    K = 16
+    launch = rollout_launcher(mb7, B, torch.float32, K)
     w, km = time_launches(launch, max(10, steps // 4), 3, 1, 100.0)
     sec["rollout_fr3_f32_K16"] = {"steps_per_launch": K, "evals_per_s": B * K * max(10, steps // 4) / w,
                                   "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", False),

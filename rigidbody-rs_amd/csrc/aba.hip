@@ -42,27 +42,15 @@ template <typename T, int N, bool FAST>
 __global__ __launch_bounds__(kBlock) void rollout_kernel(const T *__restrict__ gmdl, T *__restrict__ q,
                                                          T *__restrict__ qd, const T *__restrict__ tau_seq, T dt,
                                                          int K, T *__restrict__ traj, uint32_t B, int64_t ld) {
+    static_assert(kBlock == kRolloutBlock, "rollout LDS state is strided by the block size");
     __shared__ T mdl[N * kLinkStride];
+    __shared__ RolloutShared<T, N> sh;
     ModelStage<T, N, kBlock> st;
     st.fetch(gmdl);
-    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t off = b * (uint32_t)sizeof(T);
-    T qv[N], qdv[N];
-    if (b < B) {
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            qv[j] = ld_row(q, j * ld, off);
-            qdv[j] = ld_row(qd, j * ld, off);
-        }
-    }
     st.commit(mdl);
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= B) return;
-    rollout_eval<T, N, FAST>(mdl, qv, qdv, tau_seq, dt, K, traj, ld, off);
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        st_row(q, j * ld, off, qv[j]);
-        st_row(qd, j * ld, off, qdv[j]);
-    }
+    rollout_lane<T, N, FAST>(mdl, q, qd, tau_seq, dt, K, traj, b, ld, sh);
 }
 
 }  // namespace dev

@@ -45,7 +45,8 @@ __device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T
 
     // Pass 2: articulated inertias, leaf to root.
     reload_fence();
-    T Ur[N][3], Ul[N][3], invD[N], uu[N];
+    // Pass-3 state per joint: U/D = (dr.x, dr.y, 1; dl) -- U's own z entry is D -- and u/D.
+    T Drx[N], Dry[N], Dl[N][3], uD[N];
     ArtI<T> IA = rigid_inertia(load_link(mdl, N - 1));
     V3<T> pAn = pn[N - 1], pAf = pf[N - 1];
 #pragma unroll
@@ -54,30 +55,32 @@ __device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T
         const V3<T> ul = v3(IA.B.m[6], IA.B.m[7], IA.B.m[8]);
         const T Dinv = T(1) / IA.A.zz;
         const T u = tv[j] - pAn.z;
-        Ur[j][0] = ur.x; Ur[j][1] = ur.y; Ur[j][2] = ur.z;
-        Ul[j][0] = ul.x; Ul[j][1] = ul.y; Ul[j][2] = ul.z;
-        invD[j] = Dinv;
-        uu[j] = u;
+        Drx[j] = ur.x * Dinv; Dry[j] = ur.y * Dinv;
+        Dl[j][0] = ul.x * Dinv; Dl[j][1] = ul.y * Dinv; Dl[j][2] = ul.z * Dinv;
+        uD[j] = u * Dinv;
         if (j > 0) {
-            const V3<T> dr = v3(ur.x * Dinv, ur.y * Dinv, ur.z * Dinv);
-            const V3<T> dl = v3(ul.x * Dinv, ul.y * Dinv, ul.z * Dinv);
-            // Ia = IA - U U^T / D
+            const V3<T> dr = v3(Drx[j], Dry[j], T(1));
+            const V3<T> dl = v3(Dl[j][0], Dl[j][1], Dl[j][2]);
+            // Ia = IA - U U^T / D.  Ia S = 0 exactly (S = rot z), so Ia's rot-z row/column
+            // (A.xz, A.yz, A.zz and B's z row) are literal zeros; writing them as such lets
+            // every later product skip those terms (Featherstone 2008 §7.3).
             ArtI<T> Ia;
-            Ia.A = S3<T>{fmadd(-dr.x, ur.x, IA.A.xx), fmadd(-dr.x, ur.y, IA.A.xy), fmadd(-dr.x, ur.z, IA.A.xz),
-                         fmadd(-dr.y, ur.y, IA.A.yy), fmadd(-dr.y, ur.z, IA.A.yz), fmadd(-dr.z, ur.z, IA.A.zz)};
+            Ia.A = S3<T>{fmadd(-dr.x, ur.x, IA.A.xx), fmadd(-dr.x, ur.y, IA.A.xy), T(0),
+                         fmadd(-dr.y, ur.y, IA.A.yy), T(0), T(0)};
             const T drv[3] = {dr.x, dr.y, dr.z};
             const T ulv[3] = {ul.x, ul.y, ul.z};
 #pragma unroll
-            for (int r = 0; r < 3; ++r)
+            for (int r = 0; r < 2; ++r)
 #pragma unroll
                 for (int c = 0; c < 3; ++c) Ia.B.m[3 * r + c] = fmadd(-drv[r], ulv[c], IA.B.m[3 * r + c]);
+            Ia.B.m[6] = T(0); Ia.B.m[7] = T(0); Ia.B.m[8] = T(0);
             Ia.M = S3<T>{fmadd(-dl.x, ul.x, IA.M.xx), fmadd(-dl.x, ul.y, IA.M.xy), fmadd(-dl.x, ul.z, IA.M.xz),
                          fmadd(-dl.y, ul.y, IA.M.yy), fmadd(-dl.y, ul.z, IA.M.yz), fmadd(-dl.z, ul.z, IA.M.zz)};
-            // pa = pA + Ia c + U u / D,   c = (cw0, cw1, 0; cv0, cv1, 0)
+            // pa = pA + Ia c + U u / D,   c = (cw0, cw1, 0; cv0, cv1, 0); S^T pa = tau exactly
             const T a0 = cw0[j], a1 = cw1[j], b0 = cv0[j], b1 = cv1[j];
             V3<T> pa_n = v3(fmadd(Ia.A.xx, a0, fmadd(Ia.A.xy, a1, fmadd(Ia.B.m[0], b0, fmadd(Ia.B.m[1], b1, fmadd(dr.x, u, pAn.x))))),
                             fmadd(Ia.A.xy, a0, fmadd(Ia.A.yy, a1, fmadd(Ia.B.m[3], b0, fmadd(Ia.B.m[4], b1, fmadd(dr.y, u, pAn.y))))),
-                            fmadd(Ia.A.xz, a0, fmadd(Ia.A.yz, a1, fmadd(Ia.B.m[6], b0, fmadd(Ia.B.m[7], b1, fmadd(dr.z, u, pAn.z))))));
+                            tv[j]);
             V3<T> pa_f = v3(fmadd(Ia.B.m[0], a0, fmadd(Ia.B.m[3], a1, fmadd(Ia.M.xx, b0, fmadd(Ia.M.xy, b1, fmadd(dl.x, u, pAf.x))))),
                             fmadd(Ia.B.m[1], a0, fmadd(Ia.B.m[4], a1, fmadd(Ia.M.xy, b0, fmadd(Ia.M.yy, b1, fmadd(dl.y, u, pAf.y))))),
                             fmadd(Ia.B.m[2], a0, fmadd(Ia.B.m[5], a1, fmadd(Ia.M.xz, b0, fmadd(Ia.M.yz, b1, fmadd(dl.z, u, pAf.z))))));
@@ -111,9 +114,8 @@ __device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T
         }
         aw.x += cw0[j]; aw.y += cw1[j];
         av.x += cv0[j]; av.y += cv1[j];
-        const T dot = fmadd(Ur[j][0], aw.x, fmadd(Ur[j][1], aw.y, fmadd(Ur[j][2], aw.z,
-                      fmadd(Ul[j][0], av.x, fmadd(Ul[j][1], av.y, Ul[j][2] * av.z)))));
-        const T a = (uu[j] - dot) * invD[j];
+        const T a = uD[j] - fmadd(Drx[j], aw.x, fmadd(Dry[j], aw.y, fmadd(Dl[j][0], av.x,
+                                  fmadd(Dl[j][1], av.y, fmadd(Dl[j][2], av.z, aw.z)))));
         aw.z += a;
         out(j, a);
     }
@@ -135,46 +137,91 @@ __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, 
 }
 
 // Fused rollout (the MPC-shooting use of forward dynamics): K steps
-// of semi-implicit Euler, qd += dt * fd(q, qd, tau_k); q += dt * qd, with the state kept
-// in registers across steps.  q, qd [n][ld] are read once and overwritten with the final
-// state; tau_seq is [K][n][ld]; traj ([K][n][ld], optional) receives q after each step.
-template <typename T, int N, bool FAST>
-__device__ __forceinline__ void rollout_eval(const T *mdl, T (&qv)[N], T (&qdv)[N],
-                                             const T *__restrict__ tau_seq, T dt, int K,
-                                             T *__restrict__ traj, int64_t ld, uint32_t off) {
-    for (int k = 0; k < K; ++k) {
-        T tv[N], a[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
-        aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { a[j] = v; });
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            qdv[j] = fmadd(dt, a[j], qdv[j]);
-            qv[j] = fmadd(dt, qdv[j], qv[j]);
-        }
-        if (traj) {
-#pragma unroll
-            for (int j = 0; j < N; ++j) st_row(traj, ((int64_t)k * N + j) * ld, off, qv[j]);
-        }
-    }
+// of semi-implicit Euler, qd += dt * fd(q, qd, tau_k); q += dt * qd.  q, qd [n][ld] are
+// read once and overwritten with the final state; tau_seq is [K][n][ld]; traj
+// ([K][n][ld], optional) receives q after each step.
+//
+// Between steps the state lives in LDS (2N values per lane, row-strided by the block so
+// lanes hit distinct banks) when that fits 32 KiB per block: the dynamics already need
+// ~110 VGPRs in fp32, and holding q, qd in registers across the K loop on top of them
+// costs a wave per SIMD.  Larger chains keep the state in registers.
+constexpr int kRolloutBlock = 256;
+
+template <typename T, int N>
+constexpr bool rollout_lds_state() {
+    return 2 * N * (int)sizeof(T) * kRolloutBlock <= 32768;
 }
+
+template <typename T, int N>
+struct RolloutShared {
+    T x[rollout_lds_state<T, N>() ? 2 * N * kRolloutBlock : 1];
+};
 
 template <typename T, int N, bool FAST>
 __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T *__restrict__ qd,
                                              const T *__restrict__ tau_seq, T dt, int K, T *__restrict__ traj,
-                                             uint32_t b, int64_t ld) {
+                                             uint32_t b, int64_t ld, RolloutShared<T, N> &sh) {
     const uint32_t off = b * (uint32_t)sizeof(T);
-    T qv[N], qdv[N];
+    if constexpr (rollout_lds_state<T, N>()) {
+        T *sx = sh.x + threadIdx.x;
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-        qv[j] = ld_row(q, j * ld, off);
-        qdv[j] = ld_row(qd, j * ld, off);
-    }
-    rollout_eval<T, N, FAST>(mdl, qv, qdv, tau_seq, dt, K, traj, ld, off);
+        for (int j = 0; j < N; ++j) {
+            sx[j * kRolloutBlock] = ld_row(q, j * ld, off);
+            sx[(N + j) * kRolloutBlock] = ld_row(qd, j * ld, off);
+        }
+        for (int k = 0; k < K; ++k) {
+            T qv[N], qdv[N], tv[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-        st_row(q, j * ld, off, qv[j]);
-        st_row(qd, j * ld, off, qdv[j]);
+            for (int j = 0; j < N; ++j) {
+                qv[j] = sx[j * kRolloutBlock];
+                qdv[j] = sx[(N + j) * kRolloutBlock];
+                tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
+            }
+            // aba_eval fences memory before its last pass, so these re-read LDS.
+            aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T a) {
+                const T qdn = fmadd(dt, a, sx[(N + j) * kRolloutBlock]);
+                const T qn = fmadd(dt, qdn, sx[j * kRolloutBlock]);
+                sx[(N + j) * kRolloutBlock] = qdn;
+                sx[j * kRolloutBlock] = qn;
+                if (traj) st_row(traj, ((int64_t)k * N + j) * ld, off, qn);
+            });
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            st_row(q, j * ld, off, sx[j * kRolloutBlock]);
+            st_row(qd, j * ld, off, sx[(N + j) * kRolloutBlock]);
+        }
+    } else {
+        T qv[N], qdv[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q, j * ld, off);
+            qdv[j] = ld_row(qd, j * ld, off);
+        }
+        for (int k = 0; k < K; ++k) {
+            T tv[N], a[N];
+#pragma unroll
+            for (int j = 0; j < N; ++j) tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
+            aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { a[j] = v; });
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                qdv[j] = fmadd(dt, a[j], qdv[j]);
+                qv[j] = fmadd(dt, qdv[j], qv[j]);
+            }
+            if (traj) {
+#pragma unroll
+                for (int j = 0; j < N; ++j) st_row(traj, ((int64_t)k * N + j) * ld, off, qv[j]);
+            }
+        }
+        // Recompute the row addresses after the loop rather than holding 2N 64-bit
+        // pointers from the loads across all K steps.
+        uint32_t off2 = off;
+        asm volatile("" : "+v"(off2));
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            st_row(q, j * ld, off2, qv[j]);
+            st_row(qd, j * ld, off2, qdv[j]);
+        }
     }
 }
 

@@ -128,17 +128,21 @@ int device_consts(const Multibody *mb, const T **out) {
     return RB_OK;
 }
 
+// Resident grid-stride form of a JIT kernel (tuning.hpp policies).
+bool jit_stream(rbamd::JitKind kind, bool f64, int n) {
+    return kind == rbamd::JitKind::Rnea && rbamd::rnea_use_stream(f64, n, true);
+}
+
 // The hipRTC kernel of `kind` for this model on the current device, or nullptr (the
 // precompiled generic kernel then runs).
 const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f64, bool fast) {
     if (!rbamd::jit_enabled()) return nullptr;
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
-    const bool stream = kind == rbamd::JitKind::Rnea && rbamd::rnea_use_stream(f64, mb->model.n, true);
+    const bool stream = jit_stream(kind, f64, mb->model.n);
     const bool fst = fast && !f64;
     const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
-                            (fst ? ":fast" : ":precise") + (stream ? ":stream" : ":lane") + ":nt" +
-                            std::to_string(kind == rbamd::JitKind::Rnea ? (rbamd::tuning().rnea_nt & 3) : 0);
+                            (fst ? ":fast" : ":precise") + (stream ? ":stream" : ":lane") + rbamd::jit_tag(kind, f64, mb->model.n);
     std::lock_guard<std::mutex> lk(mb->mu);
     auto it = mb->jit.find(key);
     if (it == mb->jit.end()) {
@@ -590,7 +594,7 @@ int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int6
     if (kind < 0 || kind > 3) return -set_err(RB_ERR_ARG, "kind must be 0 rnea, 1 fd, 2 crba or 3 rollout");
     const std::string src = rbamd::jit_source(mb->model, (rbamd::JitKind)kind, f64 != 0,
                                               kind != 2 && fast_trig() && !f64,
-                                              kind == 0 && rbamd::rnea_use_stream(f64 != 0, mb->model.n, true));
+                                              jit_stream((rbamd::JitKind)kind, f64 != 0, mb->model.n));
     if (buf && cap > 0) {
         const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
         std::memcpy(buf, src.data(), n);
@@ -605,7 +609,7 @@ int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char
     std::vector<char> code;
     std::string err;
     if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && fast_trig() && !f64,
-                            kind == 0 && rbamd::rnea_use_stream(f64 != 0, mb->model.n, true),
+                            jit_stream((rbamd::JitKind)kind, f64 != 0, mb->model.n),
                             arch ? arch : "gfx950", &code, &err))
         return -set_err(RB_ERR_HIP, err);
     return (int64_t)code.size();
@@ -642,6 +646,10 @@ int rb_set_tuning(const char *key, int value) {
     else if (k == "jit") t.jit = value;
     else if (k == "rnea_tile") t.rnea_tile = value;
     else if (k == "rnea_nt") t.rnea_nt = value;
+    else if (k == "fd_nt") t.fd_nt = value;
+    else if (k == "jit_waves") t.jit_waves = value;
+    else if (k == "jit_variant") t.jit_variant = value;
+    else if (k == "opaque_consts") t.opaque_consts = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

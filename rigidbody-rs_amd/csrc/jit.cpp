@@ -43,6 +43,29 @@ std::string literal(double x, bool f64) {
 
 }  // namespace
 
+int jit_nt(JitKind kind) {
+    if (kind == JitKind::Rnea) return tuning().rnea_nt & 3;
+    if (kind == JitKind::Fd || kind == JitKind::Rollout) return tuning().fd_nt & 3;
+    return 0;
+}
+
+bool jit_opaque(JitKind kind, bool f64, int n) {
+    const int v = tuning().opaque_consts;
+    if (v >= 0) return v != 0;
+    return n <= 16 && (kind == JitKind::Rollout || (kind == JitKind::Fd && !f64));
+}
+
+int jit_waves(JitKind kind, bool f64, int n) {
+    const int v = tuning().jit_waves;
+    if (v >= 0) return v;
+    return (kind == JitKind::Rollout && !f64 && n <= 8) ? 4 : 0;
+}
+
+std::string jit_tag(JitKind kind, bool f64, int n) {
+    return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
+           std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":v" + std::to_string(tuning().jit_variant);
+}
+
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream) {
     std::vector<double> pk = m.pack_f64();
     for (int i = 0; i < m.n; ++i) {
@@ -52,7 +75,9 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     }
     const char *F = fast ? "true" : "false";
     std::ostringstream o;
-    o << "#define RB_NT " << (kind == JitKind::Rnea ? (tuning().rnea_nt & 3) : 0) << "\n";
+    o << "#define RB_NT " << jit_nt(kind) << "\n";
+    o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
+    o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
     o << (kind == JitKind::Rnea                               ? "#include \"rnea_body.hip.hpp\"\n"
           : (kind == JitKind::Fd || kind == JitKind::Rollout) ? "#include \"aba_body.hip.hpp\"\n"
                                                               : "#include \"crba_body.hip.hpp\"\n");
@@ -61,7 +86,11 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     o << "static __device__ constexpr T kModel[" << pk.size() << "] = {\n";
     for (size_t k = 0; k < pk.size(); ++k) o << "  " << literal(pk[k], f64) << ",\n";
     o << "};\n";
-    const char *head = "extern \"C\" __global__ __launch_bounds__(256) void ";
+    std::string head_s = "extern \"C\" __global__ __launch_bounds__(256) ";
+    if (const int w = jit_waves(kind, f64, m.n))
+        head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
+    head_s += "void ";
+    const char *head = head_s.c_str();
     if (kind == JitKind::Rnea) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
@@ -97,9 +126,10 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     } else if (kind == JitKind::Rollout) {
         o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
              "int K, T *__restrict__ traj, uint32_t B, int64_t ld) {\n";
+        o << "  __shared__ rbamd::dev::RolloutShared<T, N> sh;\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
-        o << "  rbamd::dev::rollout_lane<T, N, " << F << ">(kModel, q, qd, tau_seq, dt, K, traj, b, ld);\n}\n";
+        o << "  rbamd::dev::rollout_lane<T, N, " << F << ">(kModel, q, qd, tau_seq, dt, K, traj, b, ld, sh);\n}\n";
     } else {
         o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ H, uint32_t B, int64_t ld) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";

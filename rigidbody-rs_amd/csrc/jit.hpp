@@ -42,6 +42,13 @@ bool jit_tile_ok(int n, bool f64);
 // Generated HIP source for one specialised kernel (exposed for tests / inspection).
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream);
 
+// Non-temporal access bits of `kind`'s JIT source, and the cache-key suffix of every
+// tuning value that changes the source (tuning.hpp).
+int jit_nt(JitKind kind);
+bool jit_opaque(JitKind kind, bool f64, int n);
+int jit_waves(JitKind kind, bool f64, int n);
+std::string jit_tag(JitKind kind, bool f64, int n);
+
 // hipRTC compilation only (no device needed): fills `code` with the code object.
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream, const std::string &arch,
                  std::vector<char> *code, std::string *error);

@@ -159,16 +159,32 @@ __device__ __forceinline__ void stage_model(const T *__restrict__ mdl, T *smem) 
     st.commit(smem);
 }
 
+// Model-specialised kernels (RB_OPAQUE_CONSTS, jit.cpp): a compile-time model value that is
+// not 0 or +-1 is pinned to its use site through an SGPR (s_mov per use, scalar pipe),
+// so a runtime loop around the dynamics (the rollout) does not hoist ~70 literals into
+// registers for its whole lifetime.  The structural 0 / +-1 entries still fold away.
+#ifndef RB_OPAQUE_CONSTS
+#define RB_OPAQUE_CONSTS 0
+#endif
+template <typename T>
+__device__ __forceinline__ T mconst(T v) {
+    if constexpr (RB_OPAQUE_CONSTS != 0) {
+        if (__builtin_constant_p(v) && v != T(0) && v != T(1) && v != T(-1)) asm volatile("" : "+s"(v));
+    }
+    return v;
+}
+
 template <typename T>
 __device__ __forceinline__ Link<T> load_link(const T *__restrict__ mdl, int i) {
     const T *c = mdl + i * kLinkStride;
     Link<T> L;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) L.Rp.m[k] = c[kE0 + k];
-    L.p = v3(c[kP + 0], c[kP + 1], c[kP + 2]);
-    L.m = c[kM];
-    L.h = v3(c[kH + 0], c[kH + 1], c[kH + 2]);
-    L.Io = S3<T>{c[kIo + 0], c[kIo + 1], c[kIo + 2], c[kIo + 3], c[kIo + 4], c[kIo + 5]};
+    for (int k = 0; k < 9; ++k) L.Rp.m[k] = mconst(c[kE0 + k]);
+    L.p = v3(mconst(c[kP + 0]), mconst(c[kP + 1]), mconst(c[kP + 2]));
+    L.m = mconst(c[kM]);
+    L.h = v3(mconst(c[kH + 0]), mconst(c[kH + 1]), mconst(c[kH + 2]));
+    L.Io = S3<T>{mconst(c[kIo + 0]), mconst(c[kIo + 1]), mconst(c[kIo + 2]),
+                 mconst(c[kIo + 3]), mconst(c[kIo + 4]), mconst(c[kIo + 5])};
     return L;
 }
 
@@ -199,6 +215,9 @@ __device__ __forceinline__ void inertia_mul(const Link<T> &L, const V3<T> &w, co
 // 64-bit address per access.  Callers keep b * sizeof(T) < 2^32 (per-launch batch cap).
 // RB_NT (set by the hipRTC source, jit.cpp): bit 0 non-temporal row loads, bit 1
 // non-temporal row stores -- every input/output element is touched exactly once.
+#ifndef RB_VARIANT
+#define RB_VARIANT 0
+#endif
 #ifndef RB_NT
 #define RB_NT 0
 #endif

@@ -25,6 +25,10 @@ Tuning &tuning() {
         x.jit = env_int("RB_JIT", x.jit);
         x.rnea_tile = env_int("RB_RNEA_TILE", x.rnea_tile);
         x.rnea_nt = env_int("RB_RNEA_NT", x.rnea_nt);
+        x.fd_nt = env_int("RB_FD_NT", x.fd_nt);
+        x.opaque_consts = env_int("RB_OPAQUE_CONSTS", x.opaque_consts);
+        x.jit_waves = env_int("RB_JIT_WAVES", x.jit_waves);
+        x.jit_variant = env_int("RB_JIT_VARIANT", x.jit_variant);
         return x;
     }();
     return t;

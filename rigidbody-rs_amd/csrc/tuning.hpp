@@ -17,6 +17,19 @@ struct Tuning {
     // JIT RNEA: bit 0 non-temporal loads, bit 1 non-temporal stores (every element is
     // touched once; measured -5% fp32 / -8% fp64 kernel time).
     int rnea_nt = 3;
+    // JIT forward dynamics / rollout: same bits as rnea_nt (-5% fp32 FD kernel time).
+    int fd_nt = 3;
+    // JIT kernels: amdgpu_waves_per_eu occupancy target; 0 compiler's choice, -1 auto
+    // (4 for the fp32 rollout of chains up to 8 links: its K loop otherwise settles at
+    // 129+ VGPRs, one wave per SIMD fewer; 361 vs 390 us for 16 FR3 steps).
+    int jit_waves = -1;
+    // Model constants pinned per use (spatial.hip.hpp mconst): 1 on, 0 off, -1 auto = the
+    // rollout (fp32 390 vs 512 us; fp64 810 vs 995 us) and fp32 forward dynamics (33.8 vs
+    // 35.7 us) of chains up to 16 links; off for fp64 forward dynamics (90 vs 71 us), for
+    // longer chains (30-link fp32 FD: 1331 vs 333 us) and for the other kinds.
+    int opaque_consts = -1;
+    // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
+    int jit_variant = 0;
 };
 
 // Process-wide knobs, initialised from RB_RNEA_STREAM / RB_GRID_FACTOR / RB_JIT, adjustable through

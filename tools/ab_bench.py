@@ -2,7 +2,7 @@
 per cdna_hip_programming.md §5.4 rule 24.  Times the batched kernels over rotated
 input sets (> Infinity Cache) with a hipEvent pair around `steps` launches.
 
-usage: python tools/ab_bench.py [--kernel rnea|fd] [--dtype f32|f64] [--dof 7]
+usage: python tools/ab_bench.py [--kernel rnea|fd|rollout] [--dtype f32|f64] [--dof 7]
                                 [--variants 'rnea_stream=0' 'rnea_stream=1,grid_factor=2' ...]
 """
 import argparse
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--rollout-k", type=int, default=16, help="steps per launch for --kernel rollout")
     ap.add_argument("--variants", nargs="+", default=["rnea_stream=0", "rnea_stream=1"],
                     help="comma-separated rb_set_tuning key=value lists; the pseudo-key 'streams' "
                          "sets how many HIP streams the timed launches rotate over")
@@ -38,7 +39,11 @@ def main():
     mb.upload()
     per = 4 * mb.n * a.batch * es
     nsets = max(2, int(np.ceil(1.25 * (1 << 30) / per)))
-    sets = bench.make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED)
+    if a.kernel == "rollout":
+        launch = bench.rollout_launcher(mb, a.batch, dtype, a.rollout_k)
+    else:
+        sets = bench.make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED)
+        launch = bench.batch_launcher(mb, sets, a.kernel, dtype)
     lib = ffi.lib()
     res = {v: [] for v in a.variants}
     for r in range(a.rounds):
@@ -50,7 +55,7 @@ def main():
                     nstreams = int(val)
                     continue
                 assert lib.rb_set_tuning(k.encode(), int(val)) == 0, ffi.last_error()
-            _, ms = bench.run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
+            _, ms = bench.time_launches(launch, a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
             res[v].append(ms)
     out = {}
     for v, ms in res.items():
