@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1 << 20, help="configurations per GPU per step")
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
-    ap.add_argument("--kernel", choices=["rnea", "fd"], default="rnea")
+    ap.add_argument("--kernel", choices=["rnea", "fd", "rnea_fd"], default="rnea",
+                    help="rnea_fd = SURVEY §8(d) config 4: each step runs RNEA then forward dynamics on "
+                         "its torques (q, qd, qdd -> tau -> qdd'), 8·N·s bytes per configuration")
     ap.add_argument("--dof", type=int, default=7, help="7 = FR3; other values = synthetic z-chain")
     ap.add_argument("--rotate-gib", type=float, default=1.25, help="device memory the input sets span")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -86,8 +88,11 @@ def load_model(world, rank, dof):
 
 
 def make_sets(mb, B, dtype, kernel, nsets, seed):
+    """nsets independent (inputs, outputs) sets on the device.  rnea / rnea_fd read
+    (q, qd, qdd); fd reads (q, qd, tau).  rnea_fd has two outputs (tau, qdd')."""
     lim = mb.limits()
-    kinds = ("q", "qd", "qdd") if kernel == "rnea" else ("q", "qd", "tau")
+    kinds = ("q", "qd", "tau") if kernel == "fd" else ("q", "qd", "qdd")
+    nout = 2 if kernel == "rnea_fd" else 1
     sets = []
     for s in range(nsets):
         ins = []
@@ -96,10 +101,14 @@ def make_sets(mb, B, dtype, kernel, nsets, seed):
             t = torch.empty((mb.n, B), dtype=dtype, device="cuda")
             ffi.fill_uniform(t, lo, hi, seed + 1000 * s + k)
             ins.append(t)
-        out = torch.empty((mb.n, B), dtype=dtype, device="cuda")
-        sets.append((ins, out))
+        outs = [torch.empty((mb.n, B), dtype=dtype, device="cuda") for _ in range(nout)]
+        sets.append((ins, outs))
     torch.cuda.synchronize()
     return sets
+
+
+def set_bytes(n, B, esize, kernel):
+    return (8 if kernel == "rnea_fd" else 4) * n * B * esize
 
 
 def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1):
@@ -145,19 +154,30 @@ def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1):
 
 
 def batch_launcher(mb, sets, kernel, dtype):
-    """Closure issuing the rnea / fd batched entry point on input set i % len(sets)."""
+    """Closure issuing the batched entry point(s) of `kernel` on input set i % len(sets)."""
     lib = ffi.lib()
     suffix = "f32" if dtype == torch.float32 else "f64"
-    fn = getattr(lib, f"multibody_{'rnea' if kernel == 'rnea' else 'fd'}_batch_{suffix}")
-    B = sets[0][1].shape[1]
-    args = [(mb.handle, ins[0].data_ptr(), ins[1].data_ptr(), ins[2].data_ptr(), out.data_ptr(), B, B)
-            for ins, out in sets]
-    ns = len(args)
+    rnea = getattr(lib, f"multibody_rnea_batch_{suffix}")
+    fd = getattr(lib, f"multibody_fd_batch_{suffix}")
+    B = sets[0][1][0].shape[1]
+    ns = len(sets)
+    if kernel == "rnea_fd":
+        args = [((mb.handle, i[0].data_ptr(), i[1].data_ptr(), i[2].data_ptr(), o[0].data_ptr(), B, B),
+                 (mb.handle, i[0].data_ptr(), i[1].data_ptr(), o[0].data_ptr(), o[1].data_ptr(), B, B))
+                for i, o in sets]
 
-    def launch(i, sp):
-        rc = fn(*args[i % ns], sp)
-        if rc:
-            raise RuntimeError(ffi.last_error())
+        def launch(i, sp):
+            a1, a2 = args[i % ns]
+            if rnea(*a1, sp) or fd(*a2, sp):
+                raise RuntimeError(ffi.last_error())
+    else:
+        fn = rnea if kernel == "rnea" else fd
+        args = [(mb.handle, i[0].data_ptr(), i[1].data_ptr(), i[2].data_ptr(), o[0].data_ptr(), B, B)
+                for i, o in sets]
+
+        def launch(i, sp):
+            if fn(*args[i % ns], sp):
+                raise RuntimeError(ffi.last_error())
 
     return launch
 
@@ -191,35 +211,37 @@ def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, stre
 
 
 def side_workloads(mb7, a, rotate_gib):
-    """Secondary measurements (one GPU, serial launches): the other BASELINE configs."""
+    """Secondary measurements (one GPU, serial launches): the other SURVEY §8(d) configs."""
     sec = {}
-    B = a.batch
     steps = max(20, a.steps // 4)
 
-    def one(name, mb, kernel, dt_name, bytes_per_cfg):
+    def one(name, mb, kernel, dt_name, B=a.batch):
         ds = DT[dt_name]
-        per = 4 * mb.n * B * (4 if dt_name == "f32" else 8)
+        es = 4 if dt_name == "f32" else 8
+        per = set_bytes(mb.n, B, es, kernel)
         sets = make_sets(mb, B, ds, kernel, max(2, int(np.ceil(rotate_gib * (1 << 30) / per))), chains.SEED + 31)
         w, km = run_timed(mb, sets, kernel, ds, steps, 5, 1, 100.0)
-        sec[name] = {"evals_per_s": B * steps / w, "kernel_ms_avg": km,
-                     "hbm_frac": bytes_per_cfg * B / (km * 1e-3) / HBM_PEAK,
-                     "kernel_path": mb.kernel_path(kernel, dt_name == "f64")}
+        sec[name] = {"evals_per_s": B * steps / w, "kernel_ms_avg": km, "batch": B,
+                     "hbm_frac": per / (km * 1e-3) / HBM_PEAK,
+                     "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64") for k in kernel.split("_"))}
         del sets
         torch.cuda.empty_cache()
 
-    one("rnea_fr3_f64", mb7, "rnea", "f64", 224)
-    one("fd_fr3_f32", mb7, "fd", "f32", 112)            # BASELINE config 3 (ABA fp32)
-    one("fd_fr3_f64", mb7, "fd", "f64", 224)            # config 4 is rnea_f64 + fd_f64
+    one("rnea_fr3_f32_b65536", mb7, "rnea", "f32", 65536)    # config 2
+    one("fd_fr3_f32_b65536", mb7, "fd", "f32", 65536)        # config 3
+    one("rnea_fr3_f64", mb7, "rnea", "f64")
+    one("fd_fr3_f32", mb7, "fd", "f32")
+    one("fd_fr3_f64", mb7, "fd", "f64")
+    one("rnea_fd_fr3_f64_b131072", mb7, "rnea_fd", "f64", 1 << 17)  # config 4, one GPU's 2^17 shard
     mb30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     mb30.upload()
-    one("rnea_chain30_f32", mb30, "rnea", "f32", 480)   # config 5
-    # fused rollout: K forward-dynamics + Euler steps per launch, fp32, FR3
-    K = 16
-    launch = rollout_launcher(mb7, B, torch.float32, K)
-    w, km = time_launches(launch, max(10, steps // 4), 3, 1, 100.0)
-    sec["rollout_fr3_f32_K16"] = {"steps_per_launch": K, "evals_per_s": B * K * max(10, steps // 4) / w,
+    one("rnea_chain30_f32", mb30, "rnea", "f32")             # config 5
+    # fused rollout (SURVEY §8(f) rank 2): K forward-dynamics + Euler steps per launch
+    K, nl = 16, max(10, steps // 4)
+    w, km = time_launches(rollout_launcher(mb7, a.batch, torch.float32, K), nl, 3, 1, 100.0)
+    sec["rollout_fr3_f32_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
                                   "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", False),
-                                  "note": "evals = configurations x Euler steps; state stays in registers"}
+                                  "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)"}
     return sec
 
 
@@ -238,13 +260,17 @@ def cpu_baseline(n, B_sample_hint, kernel, cpu_seconds):
     cores = max(1, min(16, cores))  # the GPU box's CPU share is 16
     mbl = ([l["lower"] for l in raw["limits"]], [l["upper"] for l in raw["limits"]],
            [l["velocity"] for l in raw["limits"]], [l["effort"] for l in raw["limits"]])
-    kinds = ("q", "qd", "qdd") if kernel == "rnea" else ("q", "qd", "tau")
+    kinds = ("q", "qd", "tau") if kernel == "fd" else ("q", "qd", "qdd")
 
     def inputs(B):
         return [chains.host_uniform(n, B, *chains.input_ranges(mbl, kind), chains.SEED + k)
                 for k, kind in enumerate(kinds)]
 
-    call = om.rnea_batch if kernel == "rnea" else om.fd_batch
+    if kernel == "rnea_fd":
+        def call(q, qd, qdd, nthreads):
+            return om.fd_batch(q, qd, om.rnea_batch(q, qd, qdd, nthreads=nthreads), nthreads=nthreads)
+    else:
+        call = om.rnea_batch if kernel == "rnea" else om.fd_batch
     cal = inputs(20000)
     t = time.perf_counter()
     call(*cal, nthreads=1)
@@ -274,16 +300,17 @@ def main():
     dtype = DT[a.dtype]
     esize = 4 if a.dtype == "f32" else 8
     mb = load_model(world, rank, n)
-    per_set = 4 * n * a.batch * esize
+    per_set = set_bytes(n, a.batch, esize, a.kernel)
     nsets = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / per_set)))
     sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, rdist.rank_seed(chains.SEED, rank))
     wall, kern_avg_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms, a.streams)
     wall, kern_avg_ms = rdist.max_over_ranks([wall, kern_avg_ms], world, torch.device("cuda"))
     evals = world * a.batch * a.steps
     value = evals / wall
-    bytes_per_eval = 4 * n * esize  # q, qd, qdd|tau read + tau|qdd written
+    # q, qd, qdd|tau read + tau|qdd written per kernel; rnea_fd counts both
+    bytes_per_eval = set_bytes(n, 1, esize, a.kernel)
     achieved = bytes_per_eval * a.batch / (kern_avg_ms * 1e-3)
-    workload = f"{'rnea' if a.kernel == 'rnea' else 'fd'}_{'fr3' if n == 7 else f'chain{n}'}_{a.dtype}_b{a.batch}"
+    workload = f"{a.kernel}_{'fr3' if n == 7 else f'chain{n}'}_{a.dtype}_b{a.batch}"
     traffic = load_traffic(workload)
     line = {
         "metric": "RNEA evals/sec (fr3 7-DOF, batch 2^20) at 1/2/4/8 MI355X; % HBM roofline",
@@ -303,7 +330,7 @@ def main():
                    "batch_per_gpu": a.batch, "global_batch": a.batch * world, "dof": n,
                    "parallelism": f"dp{world} (independent shards, RCCL model broadcast)",
                    "input_sets": nsets, "rotated_bytes": nsets * per_set,
-                   "kernel_path": mb.kernel_path(a.kernel, f64=(a.dtype == "f64"))},
+                   "kernel_path": "+".join(mb.kernel_path(k, a.dtype == "f64") for k in a.kernel.split("_"))},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,

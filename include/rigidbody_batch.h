@@ -60,6 +60,20 @@ typedef enum {
  * number of revolute joints for which a kernel is compiled (multibody_supported_dofs). */
 Multibody *multibody_new_from_urdf(const char *path);
 Multibody *multibody_new_from_urdf_string(const char *xml, size_t len);
+
+/* Model-reading flags, beyond the reference.  0 = the reference's
+ * reading: top-level joints/links paired by index, fixed joints dropped, z axes only
+ * (multibody.rs:65-77, 130-138).
+ *   RB_MODEL_GENERAL_AXES: any revolute axis, motion subspace S = (axis, 0).  Identical
+ *     results for z-axis chains.  fwd_kin/jac stay in the URDF link frames.
+ *   RB_MODEL_URDF_TREE: follow joint parent/child names from the root link; fixed joints
+ *     are merged (child inertia into the parent body, origin into the next joint); the
+ *     inertial-origin rpy is honoured; revolute/continuous joints only; mimic joints and
+ *     branching trees are rejected (RB_ERR_URDF). */
+enum { RB_MODEL_GENERAL_AXES = 1, RB_MODEL_URDF_TREE = 2 };
+Multibody *multibody_new_from_urdf_ex(const char *path, unsigned flags);
+Multibody *multibody_new_from_urdf_string_ex(const char *xml, size_t len, unsigned flags);
+unsigned multibody_flags(const Multibody *mb);
 /* Packed fp64 model (bit-exact), for broadcasting one model to every rank (RCCL). */
 int64_t multibody_blob_size(const Multibody *mb);                 /* in doubles */
 int multibody_export_blob(const Multibody *mb, double *out, int64_t len);

@@ -15,14 +15,16 @@ oracle.c (which follows the reference's quaternion/isometry code path):
   CRBA-solve definition.
 
 Like the reference it injects joint motion about local z (multibody.rs:130-138)
-and applies gravity as a +9.81 z base acceleration (multibody.rs:117-120).
+and applies gravity as a +9.81 z base acceleration (multibody.rs:117-120).  With
+general=True the motion subspace is the joint's own axis, S_i = [axis_i; 0] -- the
+general-axis extension the reference does not have; this module
+is then its only independent check.
 """
 from __future__ import annotations
 
 import numpy as np
 
 G = 9.81
-S = np.array([0.0, 0.0, 1.0, 0.0, 0.0, 0.0])
 
 
 def skew(v):
@@ -77,16 +79,30 @@ def crf(v):
 
 
 class Model6:
-    def __init__(self, raw):
-        self.n = int(raw["n"])
-        self.Rp = [rpy_matrix(*raw["rpy"][i]) for i in range(self.n)]
-        self.p = [np.asarray(raw["xyz"][i], float) for i in range(self.n)]
-        self.axis = [np.asarray(raw["axis"][i], float) for i in range(self.n)]
-        self.I = []
+    def __init__(self, raw=None, general=False, frames=None):
+        """raw: urdf_model.model_raw_from_urdf output; or frames = dict(Rp [n,3,3], p [n,3],
+        axis [n,3], mass [n], com [n,3], icom [n,3,3]) (tree-mode reading)."""
+        if frames is not None:
+            self.n = len(frames["mass"])
+            self.Rp = [np.asarray(frames["Rp"][i], float) for i in range(self.n)]
+            self.p = [np.asarray(frames["p"][i], float) for i in range(self.n)]
+            self.axis = [np.asarray(frames["axis"][i], float) for i in range(self.n)]
+            self.I = [inertia6(frames["mass"][i], np.asarray(frames["com"][i], float),
+                               np.asarray(frames["icom"][i], float)) for i in range(self.n)]
+        else:
+            self.n = int(raw["n"])
+            self.Rp = [rpy_matrix(*raw["rpy"][i]) for i in range(self.n)]
+            self.p = [np.asarray(raw["xyz"][i], float) for i in range(self.n)]
+            self.axis = [np.asarray(raw["axis"][i], float) for i in range(self.n)]
+            self.I = []
+            for i in range(self.n):
+                j = raw["inertia6"][i]
+                ic = np.array([[j[0], j[1], j[2]], [j[1], j[3], j[4]], [j[2], j[4], j[5]]])
+                self.I.append(inertia6(raw["mass"][i], np.asarray(raw["com"][i], float), ic))
+        self.S = []
         for i in range(self.n):
-            j = raw["inertia6"][i]
-            ic = np.array([[j[0], j[1], j[2]], [j[1], j[3], j[4]], [j[2], j[4], j[5]]])
-            self.I.append(inertia6(raw["mass"][i], np.asarray(raw["com"][i], float), ic))
+            a = self.axis[i] / np.linalg.norm(self.axis[i]) if general else np.array([0.0, 0.0, 1.0])
+            self.S.append(np.concatenate([a, np.zeros(3)]))
 
     def poses(self, q):
         return [(self.Rp[i] @ axis_angle_matrix(self.axis[i], q[i]), self.p[i]) for i in range(self.n)]
@@ -100,13 +116,13 @@ class Model6:
         a = np.array([0, 0, 0, 0, 0, G], float)
         f = []
         for i in range(self.n):
-            vJ = S * qd[i]
+            vJ = self.S[i] * qd[i]
             v = X[i] @ v + vJ
-            a = X[i] @ a + S * qdd[i] + crm(v) @ vJ
+            a = X[i] @ a + self.S[i] * qdd[i] + crm(v) @ vJ
             f.append(self.I[i] @ a + crf(v) @ self.I[i] @ v)
         tau = np.zeros(self.n)
         for i in range(self.n - 1, -1, -1):
-            tau[i] = S @ f[i]
+            tau[i] = self.S[i] @ f[i]
             if i > 0:
                 f[i - 1] = f[i - 1] + X[i].T @ f[i]
         return tau
@@ -118,13 +134,13 @@ class Model6:
             Ic[i - 1] = Ic[i - 1] + X[i].T @ Ic[i] @ X[i]
         H = np.zeros((self.n, self.n))
         for i in range(self.n):
-            F = Ic[i] @ S
-            H[i, i] = S @ F
+            F = Ic[i] @ self.S[i]
+            H[i, i] = self.S[i] @ F
             j = i
             while j > 0:
                 F = X[j].T @ F
                 j -= 1
-                H[i, j] = H[j, i] = S @ F
+                H[i, j] = H[j, i] = self.S[j] @ F
         return H
 
     def aba(self, q, qd, tau):
@@ -133,7 +149,7 @@ class Model6:
         v, c, IA, pA = [None] * n, [None] * n, [None] * n, [None] * n
         vp = np.zeros(6)
         for i in range(n):
-            vJ = S * qd[i]
+            vJ = self.S[i] * qd[i]
             v[i] = X[i] @ vp + vJ
             c[i] = crm(v[i]) @ vJ
             IA[i] = self.I[i].copy()
@@ -141,9 +157,9 @@ class Model6:
             vp = v[i]
         U, D, u = [None] * n, np.zeros(n), np.zeros(n)
         for i in range(n - 1, -1, -1):
-            U[i] = IA[i] @ S
-            D[i] = S @ U[i]
-            u[i] = tau[i] - S @ pA[i]
+            U[i] = IA[i] @ self.S[i]
+            D[i] = self.S[i] @ U[i]
+            u[i] = tau[i] - self.S[i] @ pA[i]
             if i > 0:
                 Ia = IA[i] - np.outer(U[i], U[i]) / D[i]
                 pa = pA[i] + Ia @ c[i] + U[i] * u[i] / D[i]
@@ -154,7 +170,7 @@ class Model6:
         for i in range(n):
             a = X[i] @ ap + c[i]
             qdd[i] = (u[i] - U[i] @ a) / D[i]
-            a = a + S * qdd[i]
+            a = a + self.S[i] * qdd[i]
             ap = a
         return qdd
 
@@ -174,7 +190,7 @@ class Model6:
         for i in range(n - 1, -1, -1):
             # joint-i axis z in frame i, expressed at/in the last frame: X(R^T, p) applied to S
             X = xmotion(R.T, p)
-            sv = X @ S
+            sv = X @ self.S[i]
             J[:3, i] = sv[3:]
             J[3:, i] = sv[:3]
             Ri, pi = poses[i]

@@ -346,6 +346,62 @@ int oracle_model_from_raw(oracle_model *m, int n,
     return 0;
 }
 
+/* Rotation matrix -> unit quaternion (i, j, k, w), Shepperd's branch on the largest
+ * diagonal term; w >= 0. */
+static void quat_from_matrix(const double R[9], double q[4]) {
+    const double tr = R[0] + R[4] + R[8];
+    double i, j, k, w;
+    if (tr > 0.0) {
+        double s = sqrt(tr + 1.0) * 2.0;
+        w = 0.25 * s; i = (R[7] - R[5]) / s; j = (R[2] - R[6]) / s; k = (R[3] - R[1]) / s;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        double s = sqrt(1.0 + R[0] - R[4] - R[8]) * 2.0;
+        w = (R[7] - R[5]) / s; i = 0.25 * s; j = (R[1] + R[3]) / s; k = (R[2] + R[6]) / s;
+    } else if (R[4] > R[8]) {
+        double s = sqrt(1.0 + R[4] - R[0] - R[8]) * 2.0;
+        w = (R[2] - R[6]) / s; i = (R[1] + R[3]) / s; j = 0.25 * s; k = (R[5] + R[7]) / s;
+    } else {
+        double s = sqrt(1.0 + R[8] - R[0] - R[4]) * 2.0;
+        w = (R[3] - R[1]) / s; i = (R[2] + R[6]) / s; j = (R[5] + R[7]) / s; k = 0.25 * s;
+    }
+    double nrm = sqrt(i * i + j * j + k * k + w * w);
+    if (w < 0.0) nrm = -nrm;
+    q[0] = i / nrm; q[1] = j / nrm; q[2] = k / nrm; q[3] = w / nrm;
+}
+
+int oracle_model_from_frames(oracle_model *m, int n, const double *Rp, const double *p,
+                             const double *axis, const double *mass, const double *com,
+                             const double *icom9) {
+    if (n < 1 || n > ORACLE_MAX_DOF) return -1;
+    memset(m, 0, sizeof *m);
+    m->n = n;
+    for (int i = 0; i < n; ++i) {
+        const double *a = axis + 3 * i;
+        double an = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        if (!(an > 0.0)) return -2;
+        for (int k = 0; k < 3; ++k) m->axis[i][k] = a[k] / an;
+        quat_from_matrix(Rp + 9 * i, m->pq[i]);
+        memcpy(m->pt[i], p + 3 * i, 3 * sizeof(double));
+        inertia_t I = inertia_from_com(mass[i], com + 3 * i, icom9 + 9 * i);
+        m->mass[i] = I.mass;
+        memcpy(m->com[i], I.com, sizeof I.com);
+        memcpy(m->icom[i], I.icom, sizeof I.icom);
+        memcpy(m->io[i], I.io, sizeof I.io);
+    }
+    return 0;
+}
+
+void oracle_model_set_general_axes(oracle_model *m, int on) { m->general_axes = on != 0; }
+
+/* Motion subspace of joint i: the reference's z (spatial.rs:180-185) or the true axis. */
+static void joint_axis(const oracle_model *m, int i, double s[3]) {
+    if (m->general_axes) {
+        s[0] = m->axis[i][0]; s[1] = m->axis[i][1]; s[2] = m->axis[i][2];
+    } else {
+        s[0] = 0.0; s[1] = 0.0; s[2] = 1.0;
+    }
+}
+
 /* RevoluteJoint::parent_to_child, joint.rs:36-38, 48-50 */
 static iso3 parent_to_child(const oracle_model *m, int i, double qi) {
     iso3 r;
@@ -377,13 +433,26 @@ static void rnea_tr(const oracle_model *m, const iso3 *tr, const double *dq,
     sv6 a = {{0, 0, GRAVITY}, {0, 0, 0}};
     for (int i = 0; i < m->n; ++i) {
         v = motion_tf(&tr[i], &v);
-        v.rot[2] += dq[i];
         a = motion_tf(&tr[i], &a);
-        a.rot[2] += ddq[i];
-        a.lin[0] += v.lin[1] * dq[i];
-        a.lin[1] += -v.lin[0] * dq[i];
-        a.rot[0] += v.rot[1] * dq[i];
-        a.rot[1] += -v.rot[0] * dq[i];
+        if (!m->general_axes) {
+            /* multibody.rs:126-138, z hard-coded */
+            v.rot[2] += dq[i];
+            a.rot[2] += ddq[i];
+            a.lin[0] += v.lin[1] * dq[i];
+            a.lin[1] += -v.lin[0] * dq[i];
+            a.rot[0] += v.rot[1] * dq[i];
+            a.rot[1] += -v.rot[0] * dq[i];
+        } else {
+            /* v += S qd; a += S qdd + v x (S qd), S = (rot s, lin 0) */
+            double s[3], c[3];
+            joint_axis(m, i, s);
+            for (int k = 0; k < 3; ++k) v.rot[k] += s[k] * dq[i];
+            for (int k = 0; k < 3; ++k) a.rot[k] += s[k] * ddq[i];
+            cross3(v.lin, s, c);
+            for (int k = 0; k < 3; ++k) a.lin[k] += c[k] * dq[i];
+            cross3(v.rot, s, c);
+            for (int k = 0; k < 3; ++k) a.rot[k] += c[k] * dq[i];
+        }
         inertia_t I = body_of(m, i);
         sv6 Ia = inertia_mul(&I, &a);
         sv6 Iv = inertia_mul(&I, &v);
@@ -394,7 +463,9 @@ static void rnea_tr(const oracle_model *m, const iso3 *tr, const double *dq,
         }
     }
     for (int i = m->n - 1; i >= 0; --i) {
-        tau[i] = f[i].rot[2];
+        double s[3];
+        joint_axis(m, i, s);
+        tau[i] = m->general_axes ? s[0] * f[i].rot[0] + s[1] * f[i].rot[1] + s[2] * f[i].rot[2] : f[i].rot[2];
         if (i > 0) {
             iso3 inv;
             iso_inv(&tr[i], &inv);
@@ -423,15 +494,24 @@ void oracle_crba(const oracle_model *m, const double *q, double *H) {
     for (int c = 0; c < n; ++c)
         for (int r = 0; r < n; ++r) H[r + n * c] = (r == c) ? 1.0 : 0.0;
     inertia_t I = body_of(m, n - 1);
-    const sv6 S = {{0, 0, 0}, {0, 0, 1}}; /* BodyJacobian::revolute_z, spatial.rs:180-185 */
     for (int i = n - 1; i >= 0; --i) {
-        H[i + n * i] = I.io[8]; /* get_rotz, inertia.rs:91-93 */
+        sv6 S = {{0, 0, 0}, {0, 0, 0}}; /* BodyJacobian::revolute_z, spatial.rs:180-185 */
+        joint_axis(m, i, S.rot);
+        if (!m->general_axes) {
+            H[i + n * i] = I.io[8]; /* get_rotz, inertia.rs:91-93 */
+        } else {
+            double Is[3];
+            matvec3(I.io, S.rot, Is);
+            H[i + n * i] = S.rot[0] * Is[0] + S.rot[1] * Is[1] + S.rot[2] * Is[2];
+        }
         sv6 F = inertia_mul(&I, &S);
         for (int j = i - 1; j >= 0; --j) {
             iso3 inv;
             iso_inv(&tr[j + 1], &inv);
             F = force_tf(&inv, &F);
-            H[j + n * i] = F.rot[2];
+            double sj[3];
+            joint_axis(m, j, sj);
+            H[j + n * i] = m->general_axes ? sj[0] * F.rot[0] + sj[1] * F.rot[1] + sj[2] * F.rot[2] : F.rot[2];
         }
         if (i > 0) {
             inertia_t moved = inertia_transform(&I, &tr[i]);
@@ -459,8 +539,9 @@ void oracle_jac(const oracle_model *m, const double *q, double *J) {
     iso3 tr[ORACLE_MAX_DOF];
     get_transforms(m, q, tr);
     iso3 acc = {{0, 0, 0, 1}, {0, 0, 0}};
-    const sv6 S = {{0, 0, 0}, {0, 0, 1}};
     for (int i = m->n - 1; i >= 0; --i) {
+        sv6 S = {{0, 0, 0}, {0, 0, 0}};
+        joint_axis(m, i, S.rot);
         sv6 v = motion_tf(&acc, &S);
         for (int k = 0; k < 3; ++k) {
             J[6 * i + k] = v.lin[k];

@@ -37,6 +37,13 @@ typedef struct {
     double com[ORACLE_MAX_DOF][3];
     double icom[ORACLE_MAX_DOF][9]; /* inertia about COM, row-major */
     double io[ORACLE_MAX_DOF][9];   /* inertia about link origin, row-major */
+    /* 0: the reference's semantics -- joint poses rotate about `axis` but the motion
+     *    subspace is hard-coded to z (multibody.rs:130-138, spatial.rs:180-185).
+     * 1: general revolute axes (beyond the reference): S_i = (axis_i, 0)
+     *    in RNEA / CRBA / jac.  Identical to 0 when every axis is +z.  Parity for non-z
+     *    axes is pinned by the independent 6x6 formulation (featherstone6.py), not the
+     *    reference (which has no consistent general-axis dynamics). */
+    int general_axes;
 } oracle_model;
 
 /* Raw per-revolute-joint URDF values, 16 doubles per joint:
@@ -45,6 +52,14 @@ typedef struct {
 int oracle_model_from_raw(oracle_model *m, int n,
                           const double *xyz, const double *rpy, const double *axis,
                           const double *mass, const double *com, const double *inertia6);
+
+/* A chain given by explicit parent frames (R_p row-major 9 per link, p 3), unit-normalised
+ * axes, and bodies (mass, com, inertia about the COM row-major 9) -- the form the merged
+ * physical-tree URDF reading produces (oracle/urdf_model.py tree mode).  Returns 0. */
+int oracle_model_from_frames(oracle_model *m, int n, const double *Rp, const double *p,
+                             const double *axis, const double *mass, const double *com,
+                             const double *icom9);
+void oracle_model_set_general_axes(oracle_model *m, int on);
 
 int oracle_model_dof(const oracle_model *m);
 int oracle_model_size(void);

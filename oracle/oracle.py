@@ -48,6 +48,9 @@ def lib():
         L.oracle_crba_batch.argtypes = [ctypes.c_void_p, _dp, _dp, ctypes.c_long, ctypes.c_long, ctypes.c_int]
         L.oracle_rollout_batch.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, ctypes.c_double, ctypes.c_int, _dp,
                                            ctypes.c_long, ctypes.c_long, ctypes.c_int]
+        L.oracle_model_from_frames.restype = ctypes.c_int
+        L.oracle_model_from_frames.argtypes = [ctypes.c_void_p, ctypes.c_int] + [_dp] * 6
+        L.oracle_model_set_general_axes.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.oracle_quat_from_scaled_axis.argtypes = [_dp, _dp]
         L.oracle_quat_from_axis_angle.argtypes = [_dp, ctypes.c_double, _dp]
         L.oracle_quat_to_matrix.argtypes = [_dp, _dp]
@@ -72,17 +75,27 @@ def _c(a):
 
 
 class Model:
-    """fp64 oracle model built from raw URDF values (oracle/urdf_model.py)."""
+    """fp64 oracle model built from raw URDF values (oracle/urdf_model.py).
 
-    def __init__(self, raw):
+    general=True: motion subspace along each joint's own axis (oracle.h general_axes);
+    frames=...: the tree-mode reading (urdf_model.model_frames_from_urdf_tree)."""
+
+    def __init__(self, raw=None, general=False, frames=None):
         L = lib()
-        self.n = int(raw["n"])
         self._buf = ctypes.create_string_buffer(L.oracle_model_size())
-        arrs = [_c(raw[k]) for k in ("xyz", "rpy", "axis", "mass", "com", "inertia6")]
-        self._keep = arrs
-        rc = L.oracle_model_from_raw(self._buf, self.n, *[_p(a) for a in arrs])
+        if frames is not None:
+            self.n = int(frames["n"])
+            arrs = [_c(frames[k]) for k in ("Rp", "p", "axis", "mass", "com", "icom")]
+            self._keep = arrs
+            rc = L.oracle_model_from_frames(self._buf, self.n, *[_p(a) for a in arrs])
+        else:
+            self.n = int(raw["n"])
+            arrs = [_c(raw[k]) for k in ("xyz", "rpy", "axis", "mass", "com", "inertia6")]
+            self._keep = arrs
+            rc = L.oracle_model_from_raw(self._buf, self.n, *[_p(a) for a in arrs])
         if rc != 0:
-            raise ValueError(f"oracle_model_from_raw failed: {rc}")
+            raise ValueError(f"oracle model construction failed: {rc}")
+        L.oracle_model_set_general_axes(self._buf, int(bool(general)))
 
     @property
     def ptr(self):

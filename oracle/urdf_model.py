@@ -47,14 +47,15 @@ def parse_robot(xml_text: str):
                 mass_el = inertial.find("mass")
                 ine = inertial.find("inertia")
                 com = _vec(org.get("xyz") if org is not None else None)
+                com_rpy = _vec(org.get("rpy") if org is not None else None)
                 mass = float(mass_el.get("value")) if mass_el is not None else 0.0
                 if ine is not None:
                     i6 = [float(ine.get(k, "0")) for k in ("ixx", "ixy", "ixz", "iyy", "iyz", "izz")]
                 else:
                     i6 = [0.0] * 6
             else:
-                com, mass, i6 = [0.0] * 3, 0.0, [0.0] * 6
-            links.append({"name": el.get("name"), "mass": mass, "com": com, "inertia6": i6})
+                com, com_rpy, mass, i6 = [0.0] * 3, [0.0] * 3, 0.0, [0.0] * 6
+            links.append({"name": el.get("name"), "mass": mass, "com": com, "com_rpy": com_rpy, "inertia6": i6})
         elif el.tag == "joint":
             org = el.find("origin")
             ax = el.find("axis")
@@ -69,6 +70,7 @@ def parse_robot(xml_text: str):
                 "axis": _vec(ax.get("xyz") if ax is not None else None) if ax is not None else [1.0, 0.0, 0.0],
                 "parent": par.get("link") if par is not None else None,
                 "child": chi.get("link") if chi is not None else None,
+                "mimic": el.find("mimic") is not None,
                 "limit": None if lim is None else {k: float(lim.get(k)) for k in ("lower", "upper", "effort", "velocity") if lim.get(k) is not None},
             })
     return links, joints
@@ -101,3 +103,80 @@ def model_raw_from_urdf(xml_text: str):
 def index_pairing_matches_child(raw) -> bool:
     """the reference pairs by index; physically the body is the joint's child."""
     return list(raw["link_names"]) == list(raw["child_names"])
+
+
+# ----------------------------------------------------------------------------------
+# Physical-tree reading (RB_MODEL_URDF_TREE, SURVEY §8(f) rank 4) -- beyond the
+# reference, which pairs by index and drops fixed joints with their bodies.  Restated
+# independently of rigidbody-rs_amd/csrc/model.cpp (chain_from_tree): plain 3x3
+# matrices, inertia merged about the COM with the parallel-axis theorem.
+
+def _rpy(r, p, y):
+    cr, sr, cp, sp, cy, sy = np.cos(r), np.sin(r), np.cos(p), np.sin(p), np.cos(y), np.sin(y)
+    return (np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]]) @ np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+            @ np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]]))
+
+
+def _skew(v):
+    return np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
+
+
+def model_frames_from_urdf_tree(xml_text: str):
+    """Serial chain by joint parent/child names from the root link; fixed joints merged.
+    Returns dict(Rp [n,3,3], p [n,3], axis [n,3] (unit), mass [n], com [n,3], icom [n,3,3],
+    limits [n]) -- body i is joint i's child link plus its fixed-joint subtree."""
+    links, joints = parse_robot(xml_text)
+    by_name = {l["name"]: l for l in links}
+    children = [j["child"] for j in joints]
+    roots = [l["name"] for l in links if l["name"] not in children]
+    if len(roots) != 1:
+        raise ValueError(f"expected one root link, got {roots}")
+    out = {k: [] for k in ("Rp", "p", "axis", "mass", "com", "icom", "limits")}
+    cur, base = roots[0], True
+    while True:
+        parts, nxt = [], None  # (link, R, t) of the body's fixed subtree
+        stack = [(cur, np.eye(3), np.zeros(3))]
+        while stack:
+            ln, R, t = stack.pop()
+            parts.append((by_name[ln], R, t))
+            for j in joints:
+                if j["parent"] != ln:
+                    continue
+                if j["mimic"]:
+                    raise ValueError("mimic joint")
+                Rj, tj = R @ _rpy(*j["rpy"]), t + R @ np.asarray(j["xyz"], float)
+                if j["type"] == "fixed":
+                    stack.append((j["child"], Rj, tj))
+                elif j["type"] in ("revolute", "continuous"):
+                    if nxt is not None:
+                        raise ValueError("branching tree")
+                    nxt = (j, Rj, tj)
+                else:
+                    raise ValueError(f"joint type {j['type']}")
+        if not base:
+            m = sum(l["mass"] for l, _, _ in parts)
+            c = sum(l["mass"] * (R @ np.asarray(l["com"], float) + t) for l, R, t in parts)
+            c = c / m if m > 0 else np.zeros(3)
+            Ic = np.zeros((3, 3))
+            for l, R, t in parts:
+                i6 = l["inertia6"]
+                Il = np.array([[i6[0], i6[1], i6[2]], [i6[1], i6[3], i6[4]], [i6[2], i6[4], i6[5]]])
+                Rin = R @ _rpy(*l["com_rpy"])
+                d = R @ np.asarray(l["com"], float) + t - c
+                Ic += Rin @ Il @ Rin.T + l["mass"] * (d @ d * np.eye(3) - np.outer(d, d))
+            out["mass"].append(m)
+            out["com"].append(c)
+            out["icom"].append(Ic)
+        if nxt is None:
+            break
+        j, Rj, tj = nxt
+        a = np.asarray(j["axis"], float)
+        out["Rp"].append(Rj)
+        out["p"].append(tj)
+        out["axis"].append(a / np.linalg.norm(a))
+        out["limits"].append(j["limit"])
+        cur, base = j["child"], False
+    res = {k: np.array(v, dtype=np.float64) for k, v in out.items() if k != "limits"}
+    res["limits"] = out["limits"]
+    res["n"] = len(out["mass"])
+    return res

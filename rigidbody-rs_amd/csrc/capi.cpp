@@ -75,10 +75,10 @@ struct Multibody {
 namespace {
 
 Multibody *make(rbamd::Model &&m) {
-    if (!m.all_axes_z()) {
+    if (!m.axes_supported()) {
         set_err(RB_ERR_UNSUPPORTED,
                 "non-z joint axis: the reference injects joint motion about local z "
-                "(multibody.rs:130-138,144); only z-axis chains are supported");
+                "(multibody.rs:130-138,144); pass RB_MODEL_GENERAL_AXES for general axes");
         return nullptr;
     }
     if (!rbamd::dof_supported(m.n)) {
@@ -362,9 +362,9 @@ int crba_batch(const Multibody *mb, const T *q, T *H, int64_t batch, int64_t ld,
     });
 }
 
-Multibody *new_from_text(const std::string &xml) {
+Multibody *new_from_text(const std::string &xml, unsigned flags = 0) {
     try {
-        return make(rbamd::Model::from_urdf_text(xml));
+        return make(rbamd::Model::from_urdf_text(xml, flags));
     } catch (const std::exception &ex) {
         set_err(RB_ERR_URDF, ex.what());
         return nullptr;
@@ -517,18 +517,29 @@ double *multibody_jac(const Multibody *mb, const double *q) {
 }
 
 // ---------------------------------------------------------------- model handling
-Multibody *multibody_new_from_urdf(const char *path) {
+Multibody *multibody_new_from_urdf_ex(const char *path, unsigned flags) {
     if (!path) { set_err(RB_ERR_NULL, "NULL path"); return nullptr; }
     std::ifstream f(path, std::ios::binary);
     if (!f) { set_err(RB_ERR_URDF, std::string("cannot open URDF: ") + path); return nullptr; }
     std::stringstream ss;
     ss << f.rdbuf();
-    return new_from_text(ss.str());
+    return new_from_text(ss.str(), flags);
 }
 
-Multibody *multibody_new_from_urdf_string(const char *xml, size_t len) {
+Multibody *multibody_new_from_urdf_string_ex(const char *xml, size_t len, unsigned flags) {
     if (!xml) { set_err(RB_ERR_NULL, "NULL URDF string"); return nullptr; }
-    return new_from_text(std::string(xml, len));
+    return new_from_text(std::string(xml, len), flags);
+}
+
+Multibody *multibody_new_from_urdf(const char *path) { return multibody_new_from_urdf_ex(path, 0); }
+
+Multibody *multibody_new_from_urdf_string(const char *xml, size_t len) {
+    return multibody_new_from_urdf_string_ex(xml, len, 0);
+}
+
+unsigned multibody_flags(const Multibody *mb) {
+    if (!mb) { set_err(RB_ERR_NULL, "NULL Multibody handle"); return 0u; }
+    return mb->model.flags;
 }
 
 int64_t multibody_blob_size(const Multibody *mb) {

@@ -58,7 +58,11 @@ __global__ __launch_bounds__(kBlock) void jac_kernel(const T *__restrict__ gmdl,
     // acc = pose of the last frame in frame i, built leaf -> root (multibody.rs:97-106):
     // column i = motion transform of S_i = (0,0,1 | 0) by acc:
     //   rot = R^T z,  lin = R^T (0 - p x z) = -R^T (p.y, -p.x, 0)
-    M3<T> R{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
+    // Starts at the model tail (layout.hpp kTailOut): identity for z-axis chains, the last
+    // link's axis-frame change otherwise, so columns come out in the URDF link frame.
+    M3<T> R;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R.m[k] = gmdl[N * kLinkStride + k];
     V3<T> p = v3(T(0), T(0), T(0));
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {

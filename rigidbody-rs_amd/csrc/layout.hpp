@@ -15,6 +15,11 @@ enum : int {
     kPad = 22,  // 2 unused
 };
 
+// After the n link blocks: kTailOut scalars, the rotation R0 (row-major) that starts the
+// Jacobian's leaf->root accumulation -- identity for the reference's z-axis chains; the
+// last link's axis-frame change transposed for general axes (model.cpp pack).
+constexpr int kTailOut = 9;
+
 // Base acceleration: the reference's fictitious-gravity trick, +9.81 along base z
 // (multibody.rs:117-120).
 constexpr double kGravity = 9.81;

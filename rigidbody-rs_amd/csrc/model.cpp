@@ -64,7 +64,75 @@ void rotation_scaled_axis(const double R[9], double out[3]) {
     out[2] = a2 / n * ang;
 }
 
+void quat_from_matrix(const double R[9], double q[4]) {
+    // Shepperd: branch on the largest of (trace, diagonal) for a well-conditioned sqrt; w >= 0
+    const double tr = R[0] + R[4] + R[8];
+    double i, j, k, w;
+    if (tr > 0.0) {
+        const double s = std::sqrt(tr + 1.0) * 2.0;
+        w = 0.25 * s; i = (R[7] - R[5]) / s; j = (R[2] - R[6]) / s; k = (R[3] - R[1]) / s;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        const double s = std::sqrt(1.0 + R[0] - R[4] - R[8]) * 2.0;
+        w = (R[7] - R[5]) / s; i = 0.25 * s; j = (R[1] + R[3]) / s; k = (R[2] + R[6]) / s;
+    } else if (R[4] > R[8]) {
+        const double s = std::sqrt(1.0 + R[4] - R[0] - R[8]) * 2.0;
+        w = (R[2] - R[6]) / s; i = (R[1] + R[3]) / s; j = 0.25 * s; k = (R[5] + R[7]) / s;
+    } else {
+        const double s = std::sqrt(1.0 + R[8] - R[0] - R[4]) * 2.0;
+        w = (R[3] - R[1]) / s; i = (R[2] + R[6]) / s; j = (R[5] + R[7]) / s; k = 0.25 * s;
+    }
+    double nrm = std::sqrt(i * i + j * j + k * k + w * w);
+    if (w < 0.0) nrm = -nrm;
+    q[0] = i / nrm; q[1] = j / nrm; q[2] = k / nrm; q[3] = w / nrm;
+}
+
 namespace {
+
+// 3x3 helpers (row-major) for the host-side model build.
+void mat_mul(const double A[9], const double B[9], double C[9]) {
+    double T[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            T[3 * r + c] = A[3 * r + 0] * B[c] + A[3 * r + 1] * B[3 + c] + A[3 * r + 2] * B[6 + c];
+    std::memcpy(C, T, sizeof T);
+}
+void mat_t(const double A[9], double T[9]) {
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) T[3 * c + r] = A[3 * r + c];
+}
+void mat_vec(const double A[9], const double v[3], double o[3]) {
+    double t[3];
+    for (int r = 0; r < 3; ++r) t[r] = A[3 * r + 0] * v[0] + A[3 * r + 1] * v[1] + A[3 * r + 2] * v[2];
+    std::memcpy(o, t, sizeof t);
+}
+bool is_identity(const double R[9]) {
+    static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    return std::memcmp(R, I, sizeof I) == 0;
+}
+bool axis_is_z(const double a[3]) { return std::fabs(a[0]) <= 1e-12 && std::fabs(a[1]) <= 1e-12 && a[2] > 0.0; }
+
+// A rotation R_a with R_a e_z = a (unit): exactly the identity for +z, pi about x for -z,
+// else Rodrigues about e_z x a.
+void axis_frame(const double a[3], double Ra[9]) {
+    static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (axis_is_z(a)) {
+        std::memcpy(Ra, I, sizeof I);
+        return;
+    }
+    const double k[3] = {-a[1], a[0], 0.0};  // e_z x a, |k| = sin
+    const double s2 = k[0] * k[0] + k[1] * k[1];
+    const double c = a[2];
+    if (s2 <= 1e-24) {  // a = -z
+        const double F[9] = {1, 0, 0, 0, -1, 0, 0, 0, -1};
+        std::memcpy(Ra, F, sizeof F);
+        return;
+    }
+    const double K[9] = {0.0, -k[2], k[1], k[2], 0.0, -k[0], -k[1], k[0], 0.0};
+    double K2[9];
+    mat_mul(K, K, K2);
+    const double f = (1.0 - c) / s2;
+    for (int e = 0; e < 9; ++e) Ra[e] = I[e] + K[e] + f * K2[e];
+}
 
 // Inertia::from_com (inertia.rs:21-35): I_o = I_c + (m [c]x) [c]x^T
 void inertia_about_origin(double mass, const double c[3], const double ic[9], double io[9]) {
@@ -107,22 +175,160 @@ LinkModel link_from_urdf(const RawJoint &rj) {
 
 }  // namespace
 
-Model Model::from_urdf_text(const std::string &xml) {
+namespace {
+
+// Pose of a child frame in its parent: x_parent = R x_child + t.
+struct Frame {
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double t[3] = {0, 0, 0};
+};
+Frame compose(const Frame &a, const Frame &b) {
+    Frame o;
+    mat_mul(a.R, b.R, o.R);
+    mat_vec(a.R, b.t, o.t);
+    for (int k = 0; k < 3; ++k) o.t[k] += a.t[k];
+    return o;
+}
+Frame joint_origin(const UrdfJoint &j) {
+    Frame f;
+    rotation_from_euler(j.rpy[0], j.rpy[1], j.rpy[2], f.R);
+    std::memcpy(f.t, j.xyz, sizeof f.t);
+    return f;
+}
+
+// Rigid body accumulated about its own frame origin.
+struct Body {
+    double mass = 0.0, h[3] = {0, 0, 0}, io[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    void add(const UrdfLink &L, const Frame &T) {
+        double Rin[9], Rt[9], ic[9], tmp[9];
+        const double *J = L.inertia6;
+        const double il[9] = {J[0], J[1], J[2], J[1], J[3], J[4], J[2], J[4], J[5]};
+        rotation_from_euler(L.com_rpy[0], L.com_rpy[1], L.com_rpy[2], Rin);
+        mat_mul(T.R, Rin, Rin);  // inertial frame -> body frame
+        mat_t(Rin, Rt);
+        mat_mul(Rin, il, tmp);
+        mat_mul(tmp, Rt, ic);
+        double c[3];
+        mat_vec(T.R, L.com, c);
+        for (int k = 0; k < 3; ++k) c[k] += T.t[k];
+        double io_l[9];
+        inertia_about_origin(L.mass, c, ic, io_l);
+        for (int k = 0; k < 9; ++k) io[k] += io_l[k];
+        for (int k = 0; k < 3; ++k) h[k] += L.mass * c[k];
+        mass += L.mass;
+    }
+    void to_link(LinkModel &L) const {
+        L.mass = mass;
+        for (int k = 0; k < 3; ++k) L.com[k] = mass > 0.0 ? h[k] / mass : 0.0;
+        std::memcpy(L.io, io, sizeof L.io);
+        // I_c = I_o - m [c]x [c]x^T
+        double zero[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, P[9];
+        inertia_about_origin(mass, L.com, zero, P);
+        for (int k = 0; k < 9; ++k) L.icom[k] = io[k] - P[k];
+    }
+};
+
+bool movable(const std::string &type) { return type == "revolute" || type == "continuous"; }
+
+// kModelUrdfTree reading (see model.hpp).
+Model chain_from_tree(const UrdfRobot &robot) {
+    std::vector<int> as_child(robot.links.size(), 0);
+    auto link_index = [&](const std::string &name) {
+        for (size_t k = 0; k < robot.links.size(); ++k)
+            if (robot.links[k].name == name) return (int)k;
+        throw std::runtime_error("joint refers to unknown link '" + name + "'");
+    };
+    for (const UrdfJoint &j : robot.joints) {
+        link_index(j.parent);
+        as_child[link_index(j.child)]++;
+    }
+    int root = -1;
+    for (size_t k = 0; k < robot.links.size(); ++k) {
+        if (as_child[k] > 1) throw std::runtime_error("link '" + robot.links[k].name + "' has several parents");
+        if (as_child[k] == 0) {
+            if (root >= 0) throw std::runtime_error("URDF has several root links");
+            root = (int)k;
+        }
+    }
+    if (root < 0) throw std::runtime_error("URDF has no root link");
+    Model m;
+    int cur = root;
+    bool base = true;
+    LinkModel pending{};
+    for (;;) {
+        // the current body = link `cur` + its fixed-joint subtree; find its one movable child
+        Body body;
+        const UrdfJoint *next = nullptr;
+        Frame next_frame;
+        std::vector<std::pair<int, Frame>> stack{{cur, Frame{}}};
+        while (!stack.empty()) {
+            const auto [ln, T] = stack.back();
+            stack.pop_back();
+            body.add(robot.links[ln], T);
+            for (const UrdfJoint &j : robot.joints) {
+                if (j.parent != robot.links[ln].name) continue;
+                if (j.mimic) throw std::runtime_error("mimic joint '" + j.name + "' is not supported");
+                const Frame Tj = compose(T, joint_origin(j));
+                if (j.type == "fixed") {
+                    stack.push_back({link_index(j.child), Tj});
+                } else if (movable(j.type)) {
+                    if (next)
+                        throw std::runtime_error("branching tree at '" + robot.links[ln].name +
+                                                 "': only serial chains are supported");
+                    next = &j;
+                    next_frame = Tj;
+                } else {
+                    throw std::runtime_error("joint '" + j.name + "' of type '" + j.type + "' is not supported");
+                }
+            }
+        }
+        if (!base) {
+            body.to_link(pending);
+            m.links.push_back(pending);
+        }
+        if (!next) break;
+        pending = LinkModel{};
+        const double *a = next->axis;
+        const double an = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        if (!(an > 0.0)) throw std::runtime_error("joint '" + next->name + "' has a zero axis");
+        for (int k = 0; k < 3; ++k) pending.axis[k] = a[k] / an;
+        quat_from_matrix(next_frame.R, pending.pq);
+        std::memcpy(pending.pt, next_frame.t, sizeof pending.pt);
+        pending.lower = next->lower;
+        pending.upper = next->upper;
+        pending.velocity = next->velocity;
+        pending.effort = next->effort;
+        cur = link_index(next->child);
+        base = false;
+    }
+    return m;
+}
+
+}  // namespace
+
+Model Model::from_urdf_text(const std::string &xml, unsigned flags) {
+    if (flags & ~kModelFlagsAll) throw std::runtime_error("unknown model flags");
     UrdfRobot robot = parse_urdf(xml);
     Model m;
-    std::vector<RawJoint> chain = select_chain(robot, &m.pairing_matches_child);
-    if (chain.empty()) throw std::runtime_error("URDF has no non-fixed joint");
-    for (const RawJoint &rj : chain) m.links.push_back(link_from_urdf(rj));
+    if (flags & kModelUrdfTree) {
+        m = chain_from_tree(robot);
+    } else {
+        std::vector<RawJoint> chain = select_chain(robot, &m.pairing_matches_child);
+        for (const RawJoint &rj : chain) m.links.push_back(link_from_urdf(rj));
+    }
+    if (m.links.empty()) throw std::runtime_error("URDF has no non-fixed joint");
     m.n = (int)m.links.size();
+    m.flags = flags;
     return m;
 }
 
 std::vector<double> Model::blob() const {
     std::vector<double> b(kBlobHeader + (size_t)n * kBlobPerLink, 0.0);
     b[0] = kBlobMagic;
-    b[1] = 1.0;
+    b[1] = 2.0;
     b[2] = (double)n;
     b[3] = pairing_matches_child ? 1.0 : 0.0;
+    b[4] = (double)flags;
     for (int i = 0; i < n; ++i) {
         double *p = &b[kBlobHeader + (size_t)i * kBlobPerLink];
         const LinkModel &L = links[i];
@@ -142,7 +348,7 @@ std::vector<double> Model::blob() const {
 }
 
 Model Model::from_blob(const double *b, int64_t len) {
-    if (!b || len < kBlobHeader || b[0] != kBlobMagic || b[1] != 1.0)
+    if (!b || len < kBlobHeader || b[0] != kBlobMagic || b[1] != 2.0)
         throw std::runtime_error("not a rigidbody model blob");
     const int n = (int)b[2];
     if (n < 1 || len != kBlobHeader + (int64_t)n * kBlobPerLink)
@@ -150,6 +356,9 @@ Model Model::from_blob(const double *b, int64_t len) {
     Model m;
     m.n = n;
     m.pairing_matches_child = b[3] != 0.0;
+    if (!(b[4] >= 0.0 && b[4] <= (double)kModelFlagsAll && b[4] == (double)(unsigned)b[4]))
+        throw std::runtime_error("model blob has bad flags");
+    m.flags = (unsigned)b[4];
     m.links.resize(n);
     for (int i = 0; i < n; ++i) {
         const double *p = &b[kBlobHeader + (size_t)i * kBlobPerLink];
@@ -176,6 +385,8 @@ bool Model::all_axes_z() const {
     return true;
 }
 
+bool Model::axes_supported() const { return (flags & kModelGeneralAxes) != 0 || all_axes_z(); }
+
 double Model::total_mass() const {
     double s = 0.0;
     for (const LinkModel &L : links) s += L.mass;
@@ -185,23 +396,44 @@ double Model::total_mass() const {
 namespace {
 template <typename T>
 std::vector<T> pack(const Model &m) {
-    std::vector<T> out((size_t)m.n * kLinkStride, T(0));
+    std::vector<T> out((size_t)m.n * kLinkStride + kTailOut, T(0));
+    double Rprev[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // base frame: no axis change
     for (int i = 0; i < m.n; ++i) {
         const LinkModel &L = m.links[i];
         T *p = &out[(size_t)i * kLinkStride];
-        double R[9];
+        double R[9], Ra[9], pt[3], com[3], io[9];
         quat_to_matrix(L.pq, R);
+        axis_frame(L.axis, Ra);
+        std::memcpy(pt, L.pt, sizeof pt);
+        std::memcpy(com, L.com, sizeof com);
+        std::memcpy(io, L.io, sizeof io);
+        if (!is_identity(Rprev) || !is_identity(Ra)) {  // general axis: frame change
+            double Pt[9], At[9], tmp[9];
+            mat_t(Rprev, Pt);
+            mat_t(Ra, At);
+            mat_mul(Pt, R, tmp);
+            mat_mul(tmp, Ra, R);
+            mat_vec(Pt, L.pt, pt);
+            mat_vec(At, L.com, com);
+            mat_mul(At, L.io, tmp);
+            mat_mul(tmp, Ra, io);
+        }
+        std::memcpy(Rprev, Ra, sizeof Ra);
         for (int k = 0; k < 9; ++k) p[kE0 + k] = (T)R[k];
-        for (int k = 0; k < 3; ++k) p[kP + k] = (T)L.pt[k];
+        for (int k = 0; k < 3; ++k) p[kP + k] = (T)pt[k];
         p[kM] = (T)L.mass;
-        for (int k = 0; k < 3; ++k) p[kH + k] = (T)(L.mass * L.com[k]);
-        p[kIo + 0] = (T)L.io[0];
-        p[kIo + 1] = (T)L.io[1];
-        p[kIo + 2] = (T)L.io[2];
-        p[kIo + 3] = (T)L.io[4];
-        p[kIo + 4] = (T)L.io[5];
-        p[kIo + 5] = (T)L.io[8];
+        for (int k = 0; k < 3; ++k) p[kH + k] = (T)(L.mass * com[k]);
+        p[kIo + 0] = (T)io[0];
+        p[kIo + 1] = (T)io[1];
+        p[kIo + 2] = (T)io[2];
+        p[kIo + 3] = (T)io[4];
+        p[kIo + 4] = (T)io[5];
+        p[kIo + 5] = (T)io[8];
     }
+    // Jacobian start rotation: R_a of the last link, transposed (kinematics.hip jac_kernel)
+    T *tail = &out[(size_t)m.n * kLinkStride];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) tail[3 * r + c] = (T)Rprev[3 * c + r];
     return out;
 }
 }  // namespace

@@ -17,7 +17,7 @@
 
 namespace rbamd {
 
-constexpr int kBlobHeader = 4;    // magic, version, n, reserved
+constexpr int kBlobHeader = 5;    // magic, version, n, index-pairing flag, model flags
 constexpr int kBlobPerLink = 36;  // see Model::blob
 constexpr double kBlobMagic = 20250224.0;
 
@@ -32,19 +32,41 @@ struct LinkModel {
     double lower, upper, velocity, effort;
 };
 
+// Model-reading flags (rigidbody_batch.h RB_MODEL_*).
+enum : unsigned {
+    // Any revolute axis, with the motion subspace S = (axis, 0) -- the reference hard-codes
+    // z (multibody.rs:130-138) and is only consistent for z axes.  Identical results for
+    // z-axis chains.  Implemented by a constant per-link frame change at pack time.
+    kModelGeneralAxes = 1u,
+    // Physical URDF tree instead of the reference's index pairing (multibody.rs:70):
+    // follow joint parent/child names from the root link, merge fixed joints (their
+    // child bodies join the parent body, their origins compose into the next joint),
+    // honour the inertial-origin rpy, accept revolute/continuous joints only, reject
+    // mimic joints and branching (>1 movable subtree per body).
+    kModelUrdfTree = 2u,
+    kModelFlagsAll = 3u,
+};
+
 struct Model {
     int n = 0;
     std::vector<LinkModel> links;
     bool pairing_matches_child = true;
+    unsigned flags = 0;
 
-    static Model from_urdf_text(const std::string &xml);  // throws std::runtime_error
+    // throws std::runtime_error
+    static Model from_urdf_text(const std::string &xml, unsigned flags = 0);
     static Model from_blob(const double *blob, int64_t len);
     std::vector<double> blob() const;
 
     bool all_axes_z() const;
+    // Every axis usable under `flags`: +z always, any direction with kModelGeneralAxes.
+    bool axes_supported() const;
     double total_mass() const;
 
-    // Device constants: n * kLinkStride scalars, laid out per link as the enum above.
+    // Device constants: n * kLinkStride scalars laid out per link as layout.hpp says, then
+    // kTailOut.  A link whose axis is not +z is re-expressed in a frame whose z is its
+    // axis (R_a e_z = axis): R_p' = R_a,parent^T R_p R_a, p' = R_a,parent^T p,
+    // c' = R_a^T c, I' = R_a^T I R_a -- so the kernels' z-joint code is exact for any axis.
     std::vector<float> pack_f32() const;
     std::vector<double> pack_f64() const;
 };
@@ -54,5 +76,6 @@ void quat_from_scaled_axis(const double v[3], double out[4]);
 void quat_to_matrix(const double q[4], double R[9]);
 void rotation_from_euler(double r, double p, double y, double R[9]);
 void rotation_scaled_axis(const double R[9], double out[3]);
+void quat_from_matrix(const double R[9], double q[4]);
 
 }  // namespace rbamd

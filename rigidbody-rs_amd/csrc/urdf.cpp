@@ -156,7 +156,10 @@ UrdfRobot parse_urdf(const std::string &text) {
             UrdfLink L;
             if (const char *nm = el.attr("name")) L.name = nm;
             if (const XmlNode *in = el.child("inertial")) {
-                if (const XmlNode *o = in->child("origin")) parse_numbers(o->attr("xyz"), L.com, 3, "inertial origin xyz");
+                if (const XmlNode *o = in->child("origin")) {
+                    parse_numbers(o->attr("xyz"), L.com, 3, "inertial origin xyz");
+                    parse_numbers(o->attr("rpy"), L.com_rpy, 3, "inertial origin rpy");
+                }
                 if (const XmlNode *m = in->child("mass")) L.mass = parse_one(m->attr("value"), "mass");
                 if (const XmlNode *t = in->child("inertia")) {
                     static const char *keys[6] = {"ixx", "ixy", "ixz", "iyy", "iyz", "izz"};
@@ -176,6 +179,7 @@ UrdfRobot parse_urdf(const std::string &text) {
             if (const XmlNode *a = el.child("axis")) parse_numbers(a->attr("xyz"), J.axis, 3, "axis");
             if (const XmlNode *p = el.child("parent")) if (const char *v = p->attr("link")) J.parent = v;
             if (const XmlNode *c = el.child("child")) if (const char *v = c->attr("link")) J.child = v;
+            J.mimic = el.child("mimic") != nullptr;
             if (const XmlNode *l = el.child("limit")) {
                 if (const char *v = l->attr("lower")) J.lower = parse_one(v, "limit lower");
                 if (const char *v = l->attr("upper")) J.upper = parse_one(v, "limit upper");

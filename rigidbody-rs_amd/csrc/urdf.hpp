@@ -27,6 +27,7 @@ struct UrdfLink {
     std::string name;
     double mass = 0.0;
     double com[3] = {0, 0, 0};      // <inertial><origin xyz>; rpy ignored (joint.rs:66)
+    double com_rpy[3] = {0, 0, 0};  // <inertial><origin rpy>: used only by the tree reading
     double inertia6[6] = {0, 0, 0, 0, 0, 0}; // ixx ixy ixz iyy iyz izz
 };
 
@@ -37,6 +38,7 @@ struct UrdfJoint {
     double axis[3] = {1, 0, 0};     // URDF default when <axis> is absent
     static constexpr double kNaN = std::numeric_limits<double>::quiet_NaN();
     double lower = kNaN, upper = kNaN, effort = kNaN, velocity = kNaN;
+    bool mimic = false;             // has a <mimic> child
 };
 
 struct UrdfRobot {

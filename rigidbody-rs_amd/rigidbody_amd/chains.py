@@ -78,12 +78,76 @@ def synthetic_chain_urdf(n: int, lower=-3.141592653589793, upper=3.1415926535897
     return "\n".join(out) + "\n"
 
 
+def general_chain_urdf(n: int, seed: int = 7) -> str:
+    """Test model beyond the reference's reading, for
+    RB_MODEL_URDF_TREE | RB_MODEL_GENERAL_AXES: n revolute/continuous joints with random
+    unit axes (every 4th +z, one -z), random origins, inertial-origin rpy, a massive
+    fixed-joint link after every 3rd body, a fixed-only side branch on body 2, and a
+    fixed world->base joint.  Document order is deliberately NOT the chain order."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+
+    def inertial(mass):
+        a, b = rng.uniform(0.01, 0.05, 2)
+        c = rng.uniform(abs(a - b) + 0.005, a + b - 0.001)  # triangle inequality
+        com = rng.uniform(-0.1, 0.1, 3)
+        rpy = rng.uniform(-np.pi, np.pi, 3)
+        return ("    <inertial>\n"
+                f'      <origin rpy="{float(rpy[0])!r} {float(rpy[1])!r} {float(rpy[2])!r}" xyz="{float(com[0])!r} {float(com[1])!r} {float(com[2])!r}"/>\n'
+                f'      <mass value="{float(mass)!r}"/>\n'
+                f'      <inertia ixx="{float(a)!r}" ixy="0" ixz="0" iyy="{float(b)!r}" iyz="0" izz="{float(c)!r}"/>\n'
+                "    </inertial>")
+
+    def origin():
+        xyz = rng.uniform(-0.15, 0.15, 3)
+        rpy = rng.uniform(-np.pi, np.pi, 3)
+        return f'    <origin rpy="{float(rpy[0])!r} {float(rpy[1])!r} {float(rpy[2])!r}" xyz="{float(xyz[0])!r} {float(xyz[1])!r} {float(xyz[2])!r}"/>'
+
+    links, joints = ['  <link name="world"/>', '  <link name="base"/>'], [
+        '  <joint name="world_joint" type="fixed">\n    <origin rpy="0 0 0" xyz="0 0 0.1"/>\n'
+        '    <parent link="world"/>\n    <child link="base"/>\n  </joint>']
+    parent = "base"
+    for k in range(1, n + 1):
+        if k % 4 == 1:
+            axis = np.array([0.0, 0.0, 1.0])
+        elif k == 3:
+            axis = np.array([0.0, 0.0, -1.0])
+        else:
+            axis = rng.normal(size=3)
+            axis /= np.linalg.norm(axis) / rng.uniform(0.5, 2.0)  # not unit: the reader normalises
+        name = f"body{k}"
+        links.append(f'  <link name="{name}">\n{inertial(float(rng.uniform(0.5, 3.0)))}\n  </link>')
+        kind = "continuous" if k == 2 else "revolute"
+        lim = ('    <limit effort="40" velocity="2.5"/>' if kind == "continuous" else
+               '    <limit effort="40" lower="-2.8" upper="2.8" velocity="2.5"/>')
+        joints.append(f'  <joint name="j{k}" type="{kind}">\n{origin()}\n    <parent link="{parent}"/>\n'
+                      f'    <child link="{name}"/>\n    <axis xyz="{float(axis[0])!r} {float(axis[1])!r} {float(axis[2])!r}"/>\n'
+                      f"{lim}\n  </joint>")
+        parent = name
+        if k % 3 == 0:  # a massive fixed link between bodies: merged into body k
+            fx = f"flange{k}"
+            links.append(f'  <link name="{fx}">\n{inertial(float(rng.uniform(0.2, 1.0)))}\n  </link>')
+            joints.append(f'  <joint name="fix{k}" type="fixed">\n{origin()}\n    <parent link="{parent}"/>\n'
+                          f'    <child link="{fx}"/>\n  </joint>')
+            parent = fx
+        if k == 2:  # fixed-only side branch (a sensor): merged, not a chain branch
+            links.append(f'  <link name="sensor">\n{inertial(0.3)}\n  </link>')
+            joints.append(f'  <joint name="sensor_mount" type="fixed">\n{origin()}\n    <parent link="{name}"/>\n'
+                          '    <child link="sensor"/>\n  </joint>')
+    order = rng.permutation(len(joints))
+    return ('<?xml version="1.0"?>\n<robot name="general{n}">\n' + "\n".join(links) + "\n"
+            + "\n".join(joints[i] for i in order) + "\n</robot>\n").replace("{n}", str(n))
+
+
 def input_ranges(limits, kind: str):
-    """Per-joint (lo, hi) for kind in {'q','qd','qdd','tau'} from URDF limits."""
+    """Per-joint (lo, hi) for kind in {'q','qd','qdd','tau'} from URDF limits (a joint
+    without position limits -- continuous -- samples q in [-pi, pi])."""
+    import math
     lower, upper, vel, eff = limits
     n = len(lower)
     if kind == "q":
-        return list(lower), list(upper)
+        return ([-math.pi if math.isnan(x) else x for x in lower],
+                [math.pi if math.isnan(x) else x for x in upper])
     if kind == "qd":
         return [-v for v in vel], list(vel)
     if kind == "qdd":

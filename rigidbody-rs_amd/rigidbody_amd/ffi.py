@@ -58,6 +58,9 @@ for _n in ("multibody_fwd_kin", "multibody_jac", "multibody_crba"):
 _sig("multibody_rnea", _dp, [_vp, _dp, _dp, _dp])
 _sig("multibody_new_from_urdf", _vp, [ctypes.c_char_p])
 _sig("multibody_new_from_urdf_string", _vp, [ctypes.c_char_p, ctypes.c_size_t])
+_sig("multibody_new_from_urdf_ex", _vp, [ctypes.c_char_p, ctypes.c_uint])
+_sig("multibody_new_from_urdf_string_ex", _vp, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint])
+_sig("multibody_flags", ctypes.c_uint, [_vp])
 _sig("multibody_blob_size", _i64, [_vp])
 _sig("multibody_export_blob", ctypes.c_int, [_vp, _dp, _i64])
 _sig("multibody_new_from_blob", _vp, [_dp, _i64])
@@ -82,6 +85,7 @@ _sig("multibody_kernel_path", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int])
 _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
 KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3}
+GENERAL_AXES, URDF_TREE = 1, 2  # rigidbody_batch.h RB_MODEL_*
 for _t in ("f32", "f64"):
     _sig(f"multibody_rollout_batch_{_t}", ctypes.c_int,
          [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_int, _vp, _i64, _i64, _vp])
@@ -193,13 +197,22 @@ class Multibody:
         return cls(_lib.multibody_new())
 
     @classmethod
-    def from_urdf(cls, path):
+    def from_urdf(cls, path, flags: int = 0):
+        """flags: GENERAL_AXES | URDF_TREE (rigidbody_batch.h RB_MODEL_*); 0 = the reference's reading."""
+        if flags:
+            return cls(_lib.multibody_new_from_urdf_ex(os.fsencode(path), flags))
         return cls(_lib.multibody_new_from_urdf(os.fsencode(path)))
 
     @classmethod
-    def from_urdf_string(cls, xml: str):
+    def from_urdf_string(cls, xml: str, flags: int = 0):
         b = xml.encode()
+        if flags:
+            return cls(_lib.multibody_new_from_urdf_string_ex(b, len(b), flags))
         return cls(_lib.multibody_new_from_urdf_string(b, len(b)))
+
+    @property
+    def flags(self) -> int:
+        return int(_lib.multibody_flags(self._h))
 
     @classmethod
     def from_blob(cls, blob):

@@ -255,7 +255,7 @@ def test_jit_and_generic_kernels_agree(name, ffi, dev, fr3_text):
             _close(mb.crba_batch(q).cpu().numpy(), g["H"], 1e-9, f"crba f64 jit={jit}")
     finally:
         ffi.set_tuning("jit", 1)
-        ffi.set_tuning("rnea_tile", 1)
+        ffi.set_tuning("rnea_tile", 0)  # the library default (tuning.hpp)
 
 
 def test_tiled_kernel_partial_tiles_and_alignment(ffi, dev, fr3_text):

@@ -37,7 +37,7 @@ def main():
     es = 4 if a.dtype == "f32" else 8
     mb = ffi.Multibody.new() if a.dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(a.dof))
     mb.upload()
-    per = 4 * mb.n * a.batch * es
+    per = bench.set_bytes(mb.n, a.batch, es, a.kernel)
     nsets = max(2, int(np.ceil(1.25 * (1 << 30) / per)))
     if a.kernel == "rollout":
         launch = bench.rollout_launcher(mb, a.batch, dtype, a.rollout_k)
@@ -62,7 +62,7 @@ def main():
         med = float(np.median(ms))
         out[v] = {"ms_median": med, "ms_min": float(np.min(ms)),
                   "evals_per_s": a.batch / (med * 1e-3),
-                  "hbm_frac": 4 * mb.n * es * a.batch / (med * 1e-3) / bench.HBM_PEAK}
+                  "hbm_frac": per / (med * 1e-3) / bench.HBM_PEAK}
     print(json.dumps({"kernel": a.kernel, "dtype": a.dtype, "dof": a.dof, "batch": a.batch, "results": out}, indent=1))
 
 
