@@ -237,8 +237,9 @@ def side_workloads(mb7, a, rotate_gib):
     mb30.upload()
     one("rnea_chain30_f32", mb30, "rnea", "f32")             # config 5
     # fused rollout: K forward-dynamics + Euler steps per launch
-    K, nl = 16, max(10, steps // 4)
-    w, km = time_launches(rollout_launcher(mb7, a.batch, torch.float32, K), nl, 3, 1, 100.0)
+    # (its clock settles only after ~150 ms of this VALU-dense load: 495 -> 357 us per launch)
+    K, nl = 16, 40
+    w, km = time_launches(rollout_launcher(mb7, a.batch, torch.float32, K), nl, 3, 1, 300.0)
     sec["rollout_fr3_f32_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
                                   "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", False),
                                   "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)"}

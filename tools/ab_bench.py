@@ -60,7 +60,7 @@ def main():
     out = {}
     for v, ms in res.items():
         med = float(np.median(ms))
-        out[v] = {"ms_median": med, "ms_min": float(np.min(ms)),
+        out[v] = {"ms_median": med, "ms_min": float(np.min(ms)), "ms_rounds": [float(x) for x in ms],
                   "evals_per_s": a.batch / (med * 1e-3),
                   "hbm_frac": per / (med * 1e-3) / bench.HBM_PEAK}
     print(json.dumps({"kernel": a.kernel, "dtype": a.dtype, "dof": a.dof, "batch": a.batch, "results": out}, indent=1))

@@ -1,0 +1,68 @@
+"""Summarise rocprofv3 PMC passes of the headline kernel into profiles/.
+
+usage: python tools/traffic_summary.py GPURUN_OUT_DIR PROFILE_DIR WORKLOAD [KERNEL_REGEX]
+
+Reads <dir>/pmc_fetch/*counter_collection.csv, pmc_write/…, pmc_sq/…, pmc_grbm/… (one
+rocprofv3 --pmc pass each: FETCH_SIZE costs 3 TCC slots and WRITE_SIZE 2, so they cannot
+share a pass, MI355X_MICROARCH.md "rocprofv3 PMC slots") and writes
+  PROFILE_DIR/pmc_<pass>_summary.csv    per-counter mean / min / max / launches
+  profiles/traffic_<WORKLOAD>.json      the HBM bytes bench.py reports as roofline.traffic
+HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024): gfx950 FETCH_SIZE counts half
+the bytes of a coalesced streaming read -- calibrated on this repo's generic RNEA kernel
+(exactly 88.08 MB read -> 43 064 KB) and on the device fill (29.36 MB written -> 28 672 KB).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(d, regex):
+    import re
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    vals = {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if re.search(regex, r["Kernel_Name"]):
+                vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    src, prof, workload = sys.argv[1:4]
+    regex = sys.argv[4] if len(sys.argv) > 4 else "rb_jit_kernel"
+    os.makedirs(prof, exist_ok=True)
+    per = {}
+    for p in ("fetch", "write", "sq", "grbm"):
+        v = load(os.path.join(src, f"pmc_{p}"), regex)
+        if not v:
+            continue
+        with open(os.path.join(prof, f"pmc_{p}_summary.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["counter", "mean_per_launch", "min", "max", "launches"])
+            for k, xs in sorted(v.items()):
+                w.writerow([k, sum(xs) / len(xs), min(xs), max(xs), len(xs)])
+                per[k] = sum(xs) / len(xs)
+    n, B = 7, int(workload.rsplit("_b", 1)[1])
+    es = 4 if "_f32_" in workload else 8
+    alg = 4 * n * es * B
+    out = {"workload": workload, "kernel": f"{regex} (model-specialised RNEA)",
+           "algorithmic_bytes_per_launch": alg}
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+        hbm = 2 * per["FETCH_SIZE"] * 1024 + per["WRITE_SIZE"] * 1024
+        out.update({"bytes_per_launch": hbm, "traffic_over_algorithmic": hbm / alg,
+                    "FETCH_SIZE_KB_per_launch": per["FETCH_SIZE"], "WRITE_SIZE_KB_per_launch": per["WRITE_SIZE"]})
+    out["sq_counters_per_launch"] = {k: v for k, v in per.items() if k.startswith("SQ_")}
+    out["grbm_per_launch"] = {k: v for k, v in per.items() if k.startswith("GRBM_")}
+    out["method"] = ("rocprofv3 --pmc passes FETCH_SIZE / WRITE_SIZE / SQ_* / GRBM_* run separately on "
+                     "`bench.py --no-cpu-baseline --no-secondary`, kernels matching " + regex +
+                     ", mean over the profiled launches; bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), "
+                     "gfx950 FETCH_SIZE halving calibrated as this script's docstring says")
+    with open(os.path.join("profiles", f"traffic_{workload}.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: out[k] for k in out if k not in ("sq_counters_per_launch", "grbm_per_launch", "method")}))
+
+
+if __name__ == "__main__":
+    main()
