@@ -36,14 +36,18 @@ DT = {"f32": torch.float32, "f64": torch.float64}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000, help="timed steps (~21 ms at the headline: long enough "
+                                                                 "to average out clock transients)")
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch", type=int, default=1 << 20, help="configurations per GPU per step")
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
     ap.add_argument("--kernel", choices=["rnea", "fd", "rnea_fd"], default="rnea",
                     help="rnea_fd = SURVEY §8(d) config 4: each step runs RNEA then forward dynamics on "
                          "its torques (q, qd, qdd -> tau -> qdd'), 8·N·s bytes per configuration")
     ap.add_argument("--dof", type=int, default=7, help="7 = FR3; other values = synthetic z-chain")
+    ap.add_argument("--layout", choices=["tiled", "soa"], default="tiled",
+                    help="device array layout: tiled [B/256][n][256] (rigidbody_batch.h *_tiled entry points, "
+                         "the headline) or plain SoA rows [n][B] (reported as a secondary line)")
     ap.add_argument("--rotate-gib", type=float, default=1.25, help="device memory the input sets span")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work budget of the baseline sample")
@@ -87,9 +91,20 @@ def load_model(world, rank, dof):
     return mb
 
 
-def make_sets(mb, B, dtype, kernel, nsets, seed):
+def make_sets(mb, B, dtype, kernel, nsets, seed, pad=0, layout="soa"):
     """nsets independent (inputs, outputs) sets on the device.  rnea / rnea_fd read
-    (q, qd, qdd); fd reads (q, qd, tau).  rnea_fd has two outputs (tau, qdd')."""
+    (q, qd, qdd); fd reads (q, qd, tau).  rnea_fd has two outputs (tau, qdd').
+    pad > 0: rows are ld = B + pad elements apart ([n, ld] buffers used as [n, B] views).
+    layout "tiled": [ceil(B/256), n, 256] tensors (rigidbody_batch.h), filled with the
+    same values as the SoA sets (device fill, then rb_to_tiled)."""
+    if layout == "tiled":
+        sets = []
+        for ins, outs in make_sets(mb, B, dtype, kernel, nsets, seed):
+            sets.append(([ffi.to_tiled(t) for t in ins], [ffi.to_tiled(t) for t in outs]))
+            del ins, outs
+        torch.cuda.synchronize()
+        return sets
+    ld = B + pad
     lim = mb.limits()
     kinds = ("q", "qd", "tau") if kernel == "fd" else ("q", "qd", "qdd")
     nout = 2 if kernel == "rnea_fd" else 1
@@ -98,10 +113,10 @@ def make_sets(mb, B, dtype, kernel, nsets, seed):
         ins = []
         for k, kind in enumerate(kinds):
             lo, hi = chains.input_ranges(lim, kind)
-            t = torch.empty((mb.n, B), dtype=dtype, device="cuda")
+            t = torch.empty((mb.n, ld), dtype=dtype, device="cuda")[:, :B]
             ffi.fill_uniform(t, lo, hi, seed + 1000 * s + k)
             ins.append(t)
-        outs = [torch.empty((mb.n, B), dtype=dtype, device="cuda") for _ in range(nout)]
+        outs = [torch.empty((mb.n, ld), dtype=dtype, device="cuda")[:, :B] for _ in range(nout)]
         sets.append((ins, outs))
     torch.cuda.synchronize()
     return sets
@@ -153,17 +168,36 @@ def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1):
     return t1 - t0, e0.elapsed_time(e1) / steps
 
 
-def batch_launcher(mb, sets, kernel, dtype):
+def batch_launcher(mb, sets, kernel, dtype, layout="soa", B=None):
     """Closure issuing the batched entry point(s) of `kernel` on input set i % len(sets)."""
     lib = ffi.lib()
     suffix = "f32" if dtype == torch.float32 else "f64"
+    ns = len(sets)
+    if layout == "tiled":
+        rnea_t = getattr(lib, f"multibody_rnea_batch_tiled_{suffix}")
+        fd_t = getattr(lib, f"multibody_fd_batch_tiled_{suffix}")
+        calls = []
+        for i, o in sets:
+            p = [t.data_ptr() for t in i] + [t.data_ptr() for t in o]
+            if kernel == "rnea_fd":
+                calls.append(((rnea_t, (mb.handle, p[0], p[1], p[2], p[3], B)),
+                              (fd_t, (mb.handle, p[0], p[1], p[3], p[4], B))))
+            else:
+                calls.append(((rnea_t if kernel == "rnea" else fd_t, (mb.handle, p[0], p[1], p[2], p[3], B)),))
+
+        def launch_t(i, sp):
+            for fn, a in calls[i % ns]:
+                if fn(*a, sp):
+                    raise RuntimeError(ffi.last_error())
+
+        return launch_t
     rnea = getattr(lib, f"multibody_rnea_batch_{suffix}")
     fd = getattr(lib, f"multibody_fd_batch_{suffix}")
     B = sets[0][1][0].shape[1]
-    ns = len(sets)
+    ld = sets[0][1][0].stride(0) if sets[0][1][0].shape[0] > 1 else B
     if kernel == "rnea_fd":
-        args = [((mb.handle, i[0].data_ptr(), i[1].data_ptr(), i[2].data_ptr(), o[0].data_ptr(), B, B),
-                 (mb.handle, i[0].data_ptr(), i[1].data_ptr(), o[0].data_ptr(), o[1].data_ptr(), B, B))
+        args = [((mb.handle, i[0].data_ptr(), i[1].data_ptr(), i[2].data_ptr(), o[0].data_ptr(), B, ld),
+                 (mb.handle, i[0].data_ptr(), i[1].data_ptr(), o[0].data_ptr(), o[1].data_ptr(), B, ld))
                 for i, o in sets]
 
         def launch(i, sp):
@@ -172,7 +206,7 @@ def batch_launcher(mb, sets, kernel, dtype):
                 raise RuntimeError(ffi.last_error())
     else:
         fn = rnea if kernel == "rnea" else fd
-        args = [(mb.handle, i[0].data_ptr(), i[1].data_ptr(), i[2].data_ptr(), o[0].data_ptr(), B, B)
+        args = [(mb.handle, i[0].data_ptr(), i[1].data_ptr(), i[2].data_ptr(), o[0].data_ptr(), B, ld)
                 for i, o in sets]
 
         def launch(i, sp):
@@ -206,8 +240,8 @@ def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED):
     return launch
 
 
-def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1):
-    return time_launches(batch_launcher(mb, sets, kernel, dtype), steps, warmup, world, spinup_ms, streams)
+def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1, layout="soa", B=None):
+    return time_launches(batch_launcher(mb, sets, kernel, dtype, layout, B), steps, warmup, world, spinup_ms, streams)
 
 
 def side_workloads(mb7, a, rotate_gib):
@@ -219,9 +253,10 @@ def side_workloads(mb7, a, rotate_gib):
         ds = DT[dt_name]
         es = 4 if dt_name == "f32" else 8
         per = set_bytes(mb.n, B, es, kernel)
-        sets = make_sets(mb, B, ds, kernel, max(2, int(np.ceil(rotate_gib * (1 << 30) / per))), chains.SEED + 31)
-        w, km = run_timed(mb, sets, kernel, ds, steps, 5, 1, 100.0)
-        sec[name] = {"evals_per_s": B * steps / w, "kernel_ms_avg": km, "batch": B,
+        sets = make_sets(mb, B, ds, kernel, max(2, int(np.ceil(rotate_gib * (1 << 30) / per))), chains.SEED + 31,
+                         layout=a.layout)
+        w, km = run_timed(mb, sets, kernel, ds, steps, 5, 1, 100.0, 1, a.layout, B)
+        sec[name] = {"evals_per_s": B * steps / w, "kernel_ms_avg": km, "batch": B, "layout": a.layout,
                      "hbm_frac": per / (km * 1e-3) / HBM_PEAK,
                      "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64") for k in kernel.split("_"))}
         del sets
@@ -303,15 +338,16 @@ def main():
     mb = load_model(world, rank, n)
     per_set = set_bytes(n, a.batch, esize, a.kernel)
     nsets = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / per_set)))
-    sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, rdist.rank_seed(chains.SEED, rank))
-    wall, kern_avg_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms, a.streams)
+    sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, rdist.rank_seed(chains.SEED, rank), layout=a.layout)
+    wall, kern_avg_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms, a.streams,
+                                  a.layout, a.batch)
     wall, kern_avg_ms = rdist.max_over_ranks([wall, kern_avg_ms], world, torch.device("cuda"))
     evals = world * a.batch * a.steps
     value = evals / wall
     # q, qd, qdd|tau read + tau|qdd written per kernel; rnea_fd counts both
     bytes_per_eval = set_bytes(n, 1, esize, a.kernel)
     achieved = bytes_per_eval * a.batch / (kern_avg_ms * 1e-3)
-    workload = f"{a.kernel}_{'fr3' if n == 7 else f'chain{n}'}_{a.dtype}_b{a.batch}"
+    workload = f"{a.kernel}_{'fr3' if n == 7 else f'chain{n}'}_{a.dtype}_{a.layout}_b{a.batch}"
     traffic = load_traffic(workload)
     line = {
         "metric": "RNEA evals/sec (fr3 7-DOF, batch 2^20) at 1/2/4/8 MI355X; % HBM roofline",
@@ -327,6 +363,8 @@ def main():
         "dtype": a.dtype,
         "data": "synthetic (device splitmix64, SURVEY.md §8(d) distributions, seed 20250224)",
         "config": {"workload": workload, "kernel": a.kernel, "model": "fr3 7-DOF" if n == 7 else f"chain{n}",
+                   "layout": ("tiled [B/256][n][256] (each 256-configuration tile of all joints contiguous)"
+                              if a.layout == "tiled" else "SoA rows [n][B]"),
                    "streams": a.streams,
                    "batch_per_gpu": a.batch, "global_batch": a.batch * world, "dof": n,
                    "parallelism": f"dp{world} (independent shards, RCCL model broadcast)",
@@ -343,11 +381,19 @@ def main():
         line["cpu_baseline"] = cpu_baseline(n, a.batch, a.kernel, a.cpu_seconds)
     if rank == 0 and not a.no_secondary and world == 1 and n == 7:
         # the same workload with consecutive batches overlapped on 2 streams
-        w2, k2 = run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0, 2)
-        sec = {f"{a.kernel}_{a.dtype}_2streams": {"evals_per_s": a.batch * a.steps / w2, "step_ms_device": k2,
-                                                   "hbm_frac_effective": bytes_per_eval * a.batch / (k2 * 1e-3) / HBM_PEAK}}
+        w2, k2 = run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0, 2, a.layout, a.batch)
+        sec = {f"{a.kernel}_{a.dtype}_{a.layout}_2streams": {
+            "evals_per_s": a.batch * a.steps / w2, "step_ms_device": k2,
+            "hbm_frac_effective": bytes_per_eval * a.batch / (k2 * 1e-3) / HBM_PEAK}}
         del sets
         torch.cuda.empty_cache()
+        if a.layout != "soa":  # the same workload on plain SoA rows
+            sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED + 7)
+            w3, k3 = run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 100.0)
+            sec[f"{a.kernel}_{a.dtype}_soa"] = {"evals_per_s": a.batch * a.steps / w3, "kernel_ms_avg": k3,
+                                                "hbm_frac": bytes_per_eval * a.batch / (k3 * 1e-3) / HBM_PEAK}
+            del sets
+            torch.cuda.empty_cache()
         sec.update(side_workloads(mb, a, a.rotate_gib))
         line["secondary"] = sec
     if rank == 0:

@@ -107,13 +107,13 @@ int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char
 void multibody_result_free(double *p);
 const char *rb_last_error(void);
 const char *rb_version(void);
-/* Launch-shape knobs for A/B measurements ("rnea_stream": -1 auto / 0 / 1,
- * "grid_factor": >=1, "jit": 0/1);
- * defaults are the tuned values.  Process-wide. */
+/* Launch-shape knobs for A/B measurements (keys and defaults: INTEGRATION.md "Knobs",
+ * rigidbody-rs_amd/csrc/tuning.hpp); defaults are the tuned values.  Process-wide. */
 int rb_set_tuning(const char *key, int value);
 /* Bandwidth probe with the batched kernels' access pattern: reads rows_in SoA rows and
  * writes rows_out rows of `batch` floats (width 1/2/4: 4/8/16 B per lane; + 16 * nt with
- * nt bit 0 = non-temporal loads, bit 1 = non-temporal stores). */
+ * nt bit 0 = non-temporal loads, bit 1 = non-temporal stores, bit 2 = tiled layout: element
+ * (row r, config b) at ((b / 256) * rows + r) * 256 + b % 256, batch a multiple of 256). */
 int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
                       int width, void *stream);
 
@@ -130,6 +130,25 @@ int multibody_fd_batch_f32(const Multibody *mb, const float *q, const float *qd,
 int multibody_fd_batch_f64(const Multibody *mb, const double *q, const double *qd,
                            const double *tau, double *qdd, int64_t batch, int64_t ld,
                            void *stream);
+/* Tiled layout (same computation): every array is [ceil(batch/256)][rows][256], element
+ * (row j, configuration b) at ((b / 256) * rows + j) * 256 + b % 256, rows = n -- each
+ * 256-configuration tile of all joints contiguous.  On MI355X this reaches 5.97 TB/s on
+ * the RNEA pattern vs 4.68 TB/s for plain SoA rows (probe).  Allocate whole
+ * tiles; lanes past `batch` in the last tile are neither read nor written. */
+int multibody_rnea_batch_tiled_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                   float *tau, int64_t batch, void *stream);
+int multibody_rnea_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                   double *tau, int64_t batch, void *stream);
+int multibody_fd_batch_tiled_f32(const Multibody *mb, const float *q, const float *qd, const float *tau,
+                                 float *qdd, int64_t batch, void *stream);
+int multibody_fd_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
+                                 double *qdd, int64_t batch, void *stream);
+/* SoA [rows][ld] <-> tiled [ceil(batch/256)][rows][256] (to_tiled zero-fills the tail lanes). */
+int rb_to_tiled_f32(const float *src, int64_t ld, float *dst, int rows, int64_t batch, void *stream);
+int rb_to_tiled_f64(const double *src, int64_t ld, double *dst, int rows, int64_t batch, void *stream);
+int rb_from_tiled_f32(const float *src, float *dst, int64_t ld, int rows, int64_t batch, void *stream);
+int rb_from_tiled_f64(const double *src, double *dst, int64_t ld, int rows, int64_t batch, void *stream);
+
 /* Fused rollout for MPC shooting: K steps of semi-implicit Euler on the forward dynamics
  * above, qd += dt * qdd(q, qd, tau_k); q += dt * qd, state kept in registers.  q and qd
  * ([n][ld]) are read and overwritten with the final state; tau_seq is [K][n][ld] (step k,

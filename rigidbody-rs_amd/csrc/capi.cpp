@@ -166,31 +166,37 @@ hipError_t jit_launch(const rbamd::JitKernel *jk, hipFunction_t fn, uint32_t B, 
     return hipModuleLaunchKernel(fn, g, 1, 1, 256, 1, 1, 0, s, args, nullptr);
 }
 
+// tiled: the [ceil(B/256)][n][256] layout (kernels.hpp); the JIT lane kernels and the
+// generic lane kernels take it through their block stride; the SoA-only forms (JIT
+// grid-stride / LDS-tiled RNEA) are never chosen for it.
 template <typename T>
 hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *qdd, T *tau,
-                           uint32_t B, int64_t ld, hipStream_t s) {
+                           uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig())) {
-        void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&ld};
+    const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig());
+    if (jk && !(tiled && jk->stream)) {
+        const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
+        void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&lda, (void *)&bs};
         hipFunction_t fn = jk->function;
         const auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
-        if (jk->tile_function && rbamd::tuning().rnea_tile && a16(q) && a16(qd) && a16(qdd) && a16(tau) &&
+        if (!tiled && jk->tile_function && rbamd::tuning().rnea_tile && a16(q) && a16(qd) && a16(qdd) && a16(tau) &&
             ((uint64_t)ld * sizeof(T)) % 16 == 0)
             fn = jk->tile_function;
         return jit_launch(jk, fn, B, args, s);
     }
-    return rbamd::launch_rnea<T>(mb->model.n, mdl, q, qd, qdd, tau, B, ld, s, fast_trig());
+    return rbamd::launch_rnea<T>(mb->model.n, mdl, q, qd, qdd, tau, B, ld, s, fast_trig(), tiled);
 }
 
 template <typename T>
 hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *tau, T *qdd,
-                         uint32_t B, int64_t ld, hipStream_t s) {
+                         uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
     if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Fd, sizeof(T) == 8, fast_trig())) {
-        void *args[] = {(void *)&q, (void *)&qd, (void *)&tau, (void *)&qdd, (void *)&B, (void *)&ld};
+        const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
+        void *args[] = {(void *)&q, (void *)&qd, (void *)&tau, (void *)&qdd, (void *)&B, (void *)&lda, (void *)&bs};
         return jit_launch(jk, jk->function, B, args, s);
     }
-    return rbamd::launch_aba<T>(mb->model.n, mdl, q, qd, tau, qdd, B, ld, s, fast_trig());
+    return rbamd::launch_aba<T>(mb->model.n, mdl, q, qd, tau, qdd, B, ld, s, fast_trig(), tiled);
 }
 
 template <typename T>
@@ -302,31 +308,34 @@ int chunked(int64_t batch, L &&one) {
 
 template <typename T>
 int rnea_batch(const Multibody *mb, const T *q, const T *qd, const T *qdd, T *tau, int64_t batch,
-               int64_t ld, void *stream) {
-    int rc = check_batch(mb, batch, ld);
+               int64_t ld, void *stream, bool tiled = false) {
+    int rc = check_batch(mb, batch, tiled ? batch : ld);
     if (rc) return rc;
     if (batch == 0) return RB_OK;
     if (!q || !qd || !qdd || !tau) return set_err(RB_ERR_NULL, "NULL array");
     const T *mdl = nullptr;
     if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    const int64_t per = tiled ? mb->model.n : 1;  // element offset of configuration b0 (b0 % 256 == 0)
     return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = launch_rnea_any<T>(mb, mdl, q + b0, qd + b0, qdd + b0, tau + b0, nb, ld,
-                                          (hipStream_t)stream);
+        const int64_t o = b0 * per;
+        hipError_t e = launch_rnea_any<T>(mb, mdl, q + o, qd + o, qdd + o, tau + o, nb, ld, (hipStream_t)stream, tiled);
         return e == hipSuccess ? RB_OK : hip_err(e, "rnea launch");
     });
 }
 
 template <typename T>
 int fd_batch(const Multibody *mb, const T *q, const T *qd, const T *tau, T *qdd, int64_t batch,
-             int64_t ld, void *stream) {
-    int rc = check_batch(mb, batch, ld);
+             int64_t ld, void *stream, bool tiled = false) {
+    int rc = check_batch(mb, batch, tiled ? batch : ld);
     if (rc) return rc;
     if (batch == 0) return RB_OK;
     if (!q || !qd || !tau || !qdd) return set_err(RB_ERR_NULL, "NULL array");
     const T *mdl = nullptr;
     if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    const int64_t per = tiled ? mb->model.n : 1;
     return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = launch_fd_any<T>(mb, mdl, q + b0, qd + b0, tau + b0, qdd + b0, nb, ld, (hipStream_t)stream);
+        const int64_t o = b0 * per;
+        hipError_t e = launch_fd_any<T>(mb, mdl, q + o, qd + o, tau + o, qdd + o, nb, ld, (hipStream_t)stream, tiled);
         return e == hipSuccess ? RB_OK : hip_err(e, "aba launch");
     });
 }
@@ -642,10 +651,42 @@ const char *rb_version(void) { return RB_VERSION; }
 int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
                       int width, void *stream) {
     if (!in || !out) return set_err(RB_ERR_NULL, "NULL array");
-    if (rows_in < 1 || rows_out < 0 || batch < 0 || ld < batch || batch > kChunk || ((width & 15) != 1 && (width & 15) != 2 && (width & 15) != 4) || (width >> 4) > 3)
+    if (rows_in < 1 || rows_out < 0 || batch < 0 || ld < batch || batch > kChunk || ((width & 15) != 1 && (width & 15) != 2 && (width & 15) != 4) || (width >> 4) > 7)
         return set_err(RB_ERR_ARG, "bad probe shape");
     hipError_t e = rbamd::launch_probe_rows(in, out, rows_in, rows_out, (uint32_t)batch, ld, width, (hipStream_t)stream);
     return e == hipSuccess ? RB_OK : hip_err(e, "probe launch");
+}
+
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+int convert_tiled(const T *src, T *dst, int64_t ld, int rows, int64_t batch, void *stream, bool to) {
+    if (!src || !dst) return set_err(RB_ERR_NULL, "NULL array");
+    if (rows < 0 || batch < 0 || ld < batch) return set_err(RB_ERR_ARG, "bad layout conversion shape");
+    return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
+        hipError_t e = to ? rbamd::launch_to_tiled<T>(src + b0, ld, dst + b0 * rows, rows, nb, (hipStream_t)stream)
+                          : rbamd::launch_from_tiled<T>(src + b0 * rows, dst + b0, ld, rows, nb, (hipStream_t)stream);
+        return e == hipSuccess ? RB_OK : hip_err(e, "layout conversion");
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int rb_to_tiled_f32(const float *src, int64_t ld, float *dst, int rows, int64_t batch, void *stream) {
+    return convert_tiled<float>(src, dst, ld, rows, batch, stream, true);
+}
+int rb_to_tiled_f64(const double *src, int64_t ld, double *dst, int rows, int64_t batch, void *stream) {
+    return convert_tiled<double>(src, dst, ld, rows, batch, stream, true);
+}
+int rb_from_tiled_f32(const float *src, float *dst, int64_t ld, int rows, int64_t batch, void *stream) {
+    return convert_tiled<float>(src, dst, ld, rows, batch, stream, false);
+}
+int rb_from_tiled_f64(const double *src, double *dst, int64_t ld, int rows, int64_t batch, void *stream) {
+    return convert_tiled<double>(src, dst, ld, rows, batch, stream, false);
 }
 
 int rb_set_tuning(const char *key, int value) {
@@ -681,6 +722,22 @@ int multibody_fd_batch_f32(const Multibody *mb, const float *q, const float *qd,
 int multibody_fd_batch_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
                            double *qdd, int64_t batch, int64_t ld, void *stream) {
     return fd_batch<double>(mb, q, qd, tau, qdd, batch, ld, stream);
+}
+int multibody_rnea_batch_tiled_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                   float *tau, int64_t batch, void *stream) {
+    return rnea_batch<float>(mb, q, qd, qdd, tau, batch, 256, stream, true);
+}
+int multibody_rnea_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                   double *tau, int64_t batch, void *stream) {
+    return rnea_batch<double>(mb, q, qd, qdd, tau, batch, 256, stream, true);
+}
+int multibody_fd_batch_tiled_f32(const Multibody *mb, const float *q, const float *qd, const float *tau,
+                                 float *qdd, int64_t batch, void *stream) {
+    return fd_batch<float>(mb, q, qd, tau, qdd, batch, 256, stream, true);
+}
+int multibody_fd_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
+                                 double *qdd, int64_t batch, void *stream) {
+    return fd_batch<double>(mb, q, qd, tau, qdd, batch, 256, stream, true);
 }
 int multibody_rollout_batch_f32(const Multibody *mb, float *q, float *qd, const float *tau_seq, double dt, int K,
                                  float *traj, int64_t batch, int64_t ld, void *stream) {

@@ -91,23 +91,26 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
     head_s += "void ";
     const char *head = head_s.c_str();
+    // Lane kernels take the block stride bs (elements): 256 for SoA, N * 256 for the tiled
+    // layout (kernels.hpp); block k's arrays start at element k * bs, lane offset threadIdx.x.
     if (kind == JitKind::Rnea) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
-             "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
+             "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
-        if (stream) {
+        if (stream) {  // SoA only (capi.cpp)
             o << "  T qv[N], qdv[N], qddv[N];\n";
             o << "  rbamd::dev::load_cfg<T, N>(q, qd, qdd, ld, b * (uint32_t)sizeof(T), qv, qdv, qddv);\n";
             o << "  rbamd::dev::rnea_stream_lane<T, N, " << F
               << ">(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
         } else {
-            o << "  rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
+            o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+            o << "  rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
         }
         o << "}\n";
-        if (jit_tile_ok(m.n, f64)) {
+        if (jit_tile_ok(m.n, f64)) {  // SoA only
             o << head << "rb_jit_tile(const T *__restrict__ q, const T *__restrict__ qd, "
-                 "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld) {\n";
+                 "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
             o << "  __shared__ T tile[3 * N * 256];\n";
             o << "  const uint32_t b0 = blockIdx.x * 256u;\n";
             o << "  if (b0 + 256u <= B) {\n";
@@ -119,10 +122,11 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         }
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
-             "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld) {\n";
+             "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
-        o << "  rbamd::dev::aba_lane<T, N, " << F << ">(kModel, q, qd, tau, qdd, b, ld);\n}\n";
+        o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+        o << "  rbamd::dev::aba_lane<T, N, " << F << ">(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
     } else if (kind == JitKind::Rollout) {
         o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
              "int K, T *__restrict__ traj, uint32_t B, int64_t ld) {\n";

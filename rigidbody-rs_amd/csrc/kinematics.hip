@@ -90,6 +90,26 @@ __global__ __launch_bounds__(kBlock) void jac_kernel(const T *__restrict__ gmdl,
     }
 }
 
+// ------------------------------------------------------------------ layout conversion
+// One block per 256-configuration tile; both sides coalesced (a wave moves 64 consecutive
+// elements of one row).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void to_tiled_kernel(const T *__restrict__ src, int64_t ld,
+                                                          T *__restrict__ dst, int rows, uint32_t B) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    T *t = dst + (int64_t)blockIdx.x * rows * kBlock + threadIdx.x;
+    for (int r = 0; r < rows; ++r) t[(int64_t)r * kBlock] = b < B ? src[(int64_t)r * ld + b] : T(0);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void from_tiled_kernel(const T *__restrict__ src, T *__restrict__ dst,
+                                                            int64_t ld, int rows, uint32_t B) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= B) return;
+    const T *t = src + (int64_t)blockIdx.x * rows * kBlock + threadIdx.x;
+    for (int r = 0; r < rows; ++r) dst[(int64_t)r * ld + b] = t[(int64_t)r * kBlock];
+}
+
 // ---------------------------------------------------------------- synthetic inputs
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -172,6 +192,26 @@ hipError_t launch_fill_uniform(T *x, int rows, uint32_t B, int64_t ld, const dou
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_to_tiled(const T *src, int64_t ld, T *dst, int rows, uint32_t B, hipStream_t s) {
+    if (B == 0 || rows == 0) return hipSuccess;
+    hipLaunchKernelGGL((dev::to_tiled_kernel<T>), dim3(dev::grid_for(B)), dim3(dev::kBlock), 0, s, src, ld, dst,
+                       rows, B);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_from_tiled(const T *src, T *dst, int64_t ld, int rows, uint32_t B, hipStream_t s) {
+    if (B == 0 || rows == 0) return hipSuccess;
+    hipLaunchKernelGGL((dev::from_tiled_kernel<T>), dim3(dev::grid_for(B)), dim3(dev::kBlock), 0, s, src, dst, ld,
+                       rows, B);
+    return hipGetLastError();
+}
+
+template hipError_t launch_to_tiled<float>(const float *, int64_t, float *, int, uint32_t, hipStream_t);
+template hipError_t launch_to_tiled<double>(const double *, int64_t, double *, int, uint32_t, hipStream_t);
+template hipError_t launch_from_tiled<float>(const float *, float *, int64_t, int, uint32_t, hipStream_t);
+template hipError_t launch_from_tiled<double>(const double *, double *, int64_t, int, uint32_t, hipStream_t);
 template hipError_t launch_fwd_kin<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t);
 template hipError_t launch_jac<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t);
 template hipError_t launch_fill_uniform<float>(float *, int, uint32_t, int64_t, const double *, uint64_t, hipStream_t);

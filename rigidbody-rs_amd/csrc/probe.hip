@@ -29,17 +29,22 @@ struct VecOf<4> {
 };
 
 // All RI loads of a lane are issued before any use (compile-time row counts), as in the
-// unrolled dynamics kernels.
+// unrolled dynamics kernels.  NT bit 2 (value 4): tiled layout instead of SoA rows --
+// element (row r, config b) at ((b / 256) * R + r) * 256 + b % 256, so one 256-config tile
+// of all R rows is contiguous (ld unused).
 template <int W, int RI, int RO, int NT>
 __global__ __launch_bounds__(kBlock) void probe_rows_kernel(const float *__restrict__ in, float *__restrict__ out,
                                                            uint32_t B, int64_t ld) {
     using V = typename VecOf<W>::type;
     const uint32_t b = (blockIdx.x * kBlock + threadIdx.x) * W;
     if (b >= B) return;
+    constexpr bool kTiled = (NT & 4) != 0;
+    const int64_t tile = (int64_t)(b >> 8), lane = b & 255u;
     V x[RI];
 #pragma unroll
     for (int r = 0; r < RI; ++r) {
-        const V *p = reinterpret_cast<const V *>(in + r * ld + b);
+        const float *a = kTiled ? in + (tile * RI + r) * 256 + lane : in + r * ld + b;
+        const V *p = reinterpret_cast<const V *>(a);
         x[r] = (NT & 1) ? __builtin_nontemporal_load(p) : *p;
     }
     V acc = x[0];
@@ -47,7 +52,8 @@ __global__ __launch_bounds__(kBlock) void probe_rows_kernel(const float *__restr
     for (int r = 1; r < RI; ++r) acc = acc + x[r];
 #pragma unroll
     for (int r = 0; r < RO; ++r) {
-        V *p = reinterpret_cast<V *>(out + r * ld + b);
+        float *a = kTiled ? out + (tile * RO + r) * 256 + lane : out + r * ld + b;
+        V *p = reinterpret_cast<V *>(a);
         if (NT & 2)
             __builtin_nontemporal_store(acc, p);
         else
@@ -79,6 +85,10 @@ hipError_t probe_nt(const float *in, float *out, uint32_t B, int64_t ld, int wid
         case 1: return probe_go<RI, RO, 1>(in, out, B, ld, width, s);
         case 2: return probe_go<RI, RO, 2>(in, out, B, ld, width, s);
         case 3: return probe_go<RI, RO, 3>(in, out, B, ld, width, s);
+        case 4: return probe_go<RI, RO, 4>(in, out, B, ld, width, s);
+        case 5: return probe_go<RI, RO, 5>(in, out, B, ld, width, s);
+        case 6: return probe_go<RI, RO, 6>(in, out, B, ld, width, s);
+        case 7: return probe_go<RI, RO, 7>(in, out, B, ld, width, s);
         default: return probe_go<RI, RO, 0>(in, out, B, ld, width, s);
     }
 }
@@ -92,6 +102,7 @@ hipError_t launch_probe_rows(const float *in, float *out, int rows_in, int rows_
     const int nt = width >> 4;
     width &= 15;
     if (B % width != 0 || ld % width != 0) return hipErrorInvalidValue;
+    if ((nt & 4) && B % 256 != 0) return hipErrorInvalidValue;  // whole tiles only
     if (rows_in == 21 && rows_out == 7) return probe_nt<21, 7>(in, out, B, ld, width, nt, s);
     if (rows_in == 36 && rows_out == 12) return probe_nt<36, 12>(in, out, B, ld, width, nt, s);
     if (rows_in == 90 && rows_out == 30) return probe_nt<90, 30>(in, out, B, ld, width, nt, s);

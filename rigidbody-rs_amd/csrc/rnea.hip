@@ -12,19 +12,23 @@
 namespace rbamd {
 namespace dev {
 
-// One configuration per lane; the grid covers the batch.
+// One configuration per lane; the grid covers the batch.  Block k's arrays start at
+// element k * bstride: kBlock for SoA (x[j*ld + b]), N * kBlock for the tiled layout
+// (ld = kBlock; kernels.hpp).
 template <typename T, int N, bool FAST>
 __global__ __launch_bounds__(kBlock) void rnea_kernel(const T *__restrict__ gmdl,
                                                       const T *__restrict__ q,
                                                       const T *__restrict__ qd,
                                                       const T *__restrict__ qdd,
                                                       T *__restrict__ tau, uint32_t B,
-                                                      int64_t ld) {
+                                                      int64_t ld, int64_t bstride) {
     __shared__ T mdl[N * kLinkStride];
     ModelStage<T, N, kBlock> st;
     st.fetch(gmdl);
+    const int64_t o = (int64_t)blockIdx.x * bstride;
+    q += o; qd += o; qdd += o; tau += o;
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t off = b * (uint32_t)sizeof(T);
+    const uint32_t off = threadIdx.x * (uint32_t)sizeof(T);
     T qv[N], qdv[N], qddv[N];
     if (b < B) load_cfg<T, N>(q, qd, qdd, ld, off, qv, qdv, qddv);
     st.commit(mdl);
@@ -57,28 +61,33 @@ __global__ __launch_bounds__(kBlock) void rnea_stream_kernel(const T *__restrict
 namespace {
 template <typename T, int N, bool F>
 hipError_t rnea_go(const T *mdl, const T *q, const T *qd, const T *qdd, T *tau, uint32_t B, int64_t ld,
-                   hipStream_t s) {
+                   hipStream_t s, bool tiled) {
     const Tuning &tn = tuning();
     const unsigned full = dev::grid_for(B);
-    const bool stream = rnea_use_stream(sizeof(T) == 8, N, false);
-    auto kfn = stream ? dev::rnea_stream_kernel<T, N, F> : dev::rnea_kernel<T, N, F>;
-    const unsigned g = stream ? stream_grid((const void *)kfn, dev::kBlock, full, tn.grid_factor) : full;
-    hipLaunchKernelGGL(kfn, dim3(g), dim3(dev::kBlock), 0, s, mdl, q, qd, qdd, tau, B, ld);
+    if (!tiled && rnea_use_stream(sizeof(T) == 8, N, false)) {
+        auto kfn = dev::rnea_stream_kernel<T, N, F>;
+        const unsigned g = stream_grid((const void *)kfn, dev::kBlock, full, tn.grid_factor);
+        hipLaunchKernelGGL(kfn, dim3(g), dim3(dev::kBlock), 0, s, mdl, q, qd, qdd, tau, B, ld);
+    } else {
+        const int64_t bs = tiled ? (int64_t)N * dev::kBlock : dev::kBlock;
+        hipLaunchKernelGGL((dev::rnea_kernel<T, N, F>), dim3(full), dim3(dev::kBlock), 0, s, mdl, q, qd, qdd, tau,
+                           B, tiled ? (int64_t)dev::kBlock : ld, bs);
+    }
     return hipGetLastError();
 }
 }  // namespace
 
 template <typename T>
 hipError_t launch_rnea(int n, const T *mdl, const T *q, const T *qd, const T *qdd, T *tau,
-                       uint32_t B, int64_t ld, hipStream_t s, bool fast) {
+                       uint32_t B, int64_t ld, hipStream_t s, bool fast, bool tiled) {
     if (B == 0) return hipSuccess;
     switch (n) {
 #define RB_CASE(N)                                                                              \
     case N:                                                                                     \
         if constexpr (sizeof(T) == 4) {                                                          \
-            if (fast) return rnea_go<T, N, true>(mdl, q, qd, qdd, tau, B, ld, s);                \
+            if (fast) return rnea_go<T, N, true>(mdl, q, qd, qdd, tau, B, ld, s, tiled);                \
         }                                                                                        \
-        return rnea_go<T, N, false>(mdl, q, qd, qdd, tau, B, ld, s);
+        return rnea_go<T, N, false>(mdl, q, qd, qdd, tau, B, ld, s, tiled);
         RB_FOR_EACH_DOF(RB_CASE)
 #undef RB_CASE
         default:
@@ -86,7 +95,7 @@ hipError_t launch_rnea(int n, const T *mdl, const T *q, const T *qd, const T *qd
     }
 }
 
-template hipError_t launch_rnea<float>(int, const float *, const float *, const float *, const float *, float *, uint32_t, int64_t, hipStream_t, bool);
-template hipError_t launch_rnea<double>(int, const double *, const double *, const double *, const double *, double *, uint32_t, int64_t, hipStream_t, bool);
+template hipError_t launch_rnea<float>(int, const float *, const float *, const float *, const float *, float *, uint32_t, int64_t, hipStream_t, bool, bool);
+template hipError_t launch_rnea<double>(int, const double *, const double *, const double *, const double *, double *, uint32_t, int64_t, hipStream_t, bool, bool);
 
 }  // namespace rbamd

@@ -92,6 +92,12 @@ for _t in ("f32", "f64"):
 _sig("rb_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
 _sig("rb_probe_rows_f32", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _i64, _i64, ctypes.c_int, _vp])
 _sig("multibody_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
+for _t in ("f32", "f64"):
+    _sig(f"multibody_rnea_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp])
+    _sig(f"multibody_fd_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp])
+    _sig(f"rb_to_tiled_{_t}", ctypes.c_int, [_vp, _i64, _vp, ctypes.c_int, _i64, _vp])
+    _sig(f"rb_from_tiled_{_t}", ctypes.c_int, [_vp, _vp, _i64, ctypes.c_int, _i64, _vp])
+TILE = 256  # configurations per tile of the tiled layout (rigidbody_batch.h)
 
 
 class RigidBodyError(RuntimeError):
@@ -328,6 +334,33 @@ class Multibody:
                   _stream_ptr(stream)), "fd_batch")
         return out
 
+    # ---- tiled layout [ceil(B/256), n, 256] (rigidbody_batch.h) ----------------------
+    def _tiled(self, t, name, B, dtype=None):
+        T = (B + TILE - 1) // TILE
+        if not isinstance(t, torch.Tensor) or not t.is_cuda:
+            raise TypeError(f"{name} must be a CUDA (HIP) torch tensor of shape [tiles, n, 256]")
+        if tuple(t.shape) != (T, self.n, TILE) or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous [{T}, {self.n}, {TILE}] tensor for batch {B}")
+        if dtype is not None and t.dtype != dtype:
+            raise TypeError(f"{name} has dtype {t.dtype}, expected {dtype}")
+        return t
+
+    def _tiled_call(self, kind, a, b, c, B, out, stream):
+        a = self._tiled(a, "arg0", B)
+        b, c = self._tiled(b, "arg1", B, a.dtype), self._tiled(c, "arg2", B, a.dtype)
+        out = torch.empty_like(a) if out is None else self._tiled(out, "out", B, a.dtype)
+        fn = getattr(_lib, f"multibody_{kind}_batch_tiled_{_TORCH_SUFFIX[a.dtype]}")
+        _check(fn(self._h, a.data_ptr(), b.data_ptr(), c.data_ptr(), out.data_ptr(), B, _stream_ptr(stream)),
+               f"{kind}_batch_tiled")
+        return out
+
+    def rnea_batch_tiled(self, q, qd, qdd, B, out=None, stream=None):
+        """RNEA on tiled [ceil(B/256), n, 256] tensors (see to_tiled)."""
+        return self._tiled_call("rnea", q, qd, qdd, B, out, stream)
+
+    def fd_batch_tiled(self, q, qd, tau, B, out=None, stream=None):
+        return self._tiled_call("fd", q, qd, tau, B, out, stream)
+
     def rollout_batch(self, q, qd, tau_seq, dt, traj=False, stream=None):
         """K fused forward-dynamics + semi-implicit Euler steps, in place on q and qd
         ([n, B] CUDA tensors); tau_seq [K, n, B].  Returns the trajectory [K, n, B] of q
@@ -394,6 +427,29 @@ class Multibody:
         _check(_lib.multibody_fd_batch_host_f64(self._h, *[a.ctypes.data_as(_dp) for a in arrs],
                                                 out.ctypes.data_as(_dp), B), "fd_batch_host")
         return out
+
+
+def to_tiled(x, stream=None):
+    """[rows, B] SoA CUDA tensor -> new [ceil(B/256), rows, 256] tiled tensor (rb_to_tiled_*)."""
+    if not isinstance(x, torch.Tensor) or not x.is_cuda or x.dim() != 2 or (x.shape[1] > 1 and x.stride(1) != 1):
+        raise TypeError("to_tiled needs a CUDA tensor [rows, B] contiguous along B")
+    rows, B = x.shape
+    out = torch.empty(((B + TILE - 1) // TILE, rows, TILE), dtype=x.dtype, device=x.device)
+    fn = getattr(_lib, f"rb_to_tiled_{_TORCH_SUFFIX[x.dtype]}")
+    _check(fn(x.data_ptr(), _ld(x), out.data_ptr(), rows, B, _stream_ptr(stream)), "to_tiled")
+    return out
+
+
+def from_tiled(t, B, stream=None):
+    """[ceil(B/256), rows, 256] tiled tensor -> new [rows, B] SoA tensor (rb_from_tiled_*)."""
+    if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dim() != 3 or t.shape[2] != TILE or \
+            t.shape[0] != (B + TILE - 1) // TILE or not t.is_contiguous():
+        raise TypeError(f"from_tiled needs a contiguous CUDA tensor [ceil(B/256), rows, 256] for B={B}")
+    rows = t.shape[1]
+    out = torch.empty((rows, B), dtype=t.dtype, device=t.device)
+    fn = getattr(_lib, f"rb_from_tiled_{_TORCH_SUFFIX[t.dtype]}")
+    _check(fn(t.data_ptr(), out.data_ptr(), max(B, 1), rows, B, _stream_ptr(stream)), "from_tiled")
+    return out
 
 
 def fill_uniform(t, lo, hi, seed, stream=None):

@@ -338,3 +338,37 @@ def test_rollout_vs_oracle(name, ffi, dev, fr3_text):
     qd = _t(g["qd"], dev)
     assert mb.rollout_batch(q, qd, torch.as_tensor(tau_seq, device=dev), dt) is None
     _close(q.cpu().numpy(), q_ref, 1e-9, "rollout q (no traj)")
+
+
+# ------------------------------------------------------------ tiled layout
+@pytest.mark.parametrize("name", ["fr3_golden.npz", "chain12_golden.npz"])
+def test_tiled_layout_matches_soa_bitwise(name, ffi, dev, fr3_text):
+    """The tiled [ceil(B/256), n, 256] entry points run the same lane arithmetic as the
+    SoA ones: outputs are bit-identical (JIT and generic kernels, fp32 and fp64, ragged
+    batches), the layout conversions are exact round trips, and the oracle agrees."""
+    mb = ffi.Multibody.from_urdf_string(_model_xml(name, fr3_text))
+    om = _oracle(_model_xml(name, fr3_text))
+    n = mb.n
+    try:
+        for jit in (1, 0):
+            ffi.set_tuning("jit", jit)
+            for B in (1, 255, 256, 1000, 65536 + 3):
+                rng = np.random.default_rng(B)
+                q, qd, qdd = (rng.uniform(-2, 2, (n, B)) for _ in range(3))
+                for dt in (torch.float64, torch.float32):
+                    x = [_t(a, dev, dt) for a in (q, qd, qdd)]
+                    xt = [ffi.to_tiled(a) for a in x]
+                    assert all(torch.equal(ffi.from_tiled(a, B), b) for a, b in zip(xt, x))
+                    tau = mb.rnea_batch(*x)
+                    tau_t = ffi.from_tiled(mb.rnea_batch_tiled(*xt, B), B)
+                    assert torch.equal(tau, tau_t), (jit, B, dt)
+                    qdd2 = mb.fd_batch(x[0], x[1], tau)
+                    qdd2_t = ffi.from_tiled(mb.fd_batch_tiled(xt[0], xt[1], ffi.to_tiled(tau), B), B)
+                    assert torch.equal(qdd2, qdd2_t), (jit, B, dt)
+                    if dt == torch.float64 and B <= 1000:
+                        _close(tau_t.cpu().numpy(), om.rnea_batch(q, qd, qdd), 1e-9, f"tiled rnea B={B}")
+                        _close(qdd2_t.cpu().numpy(), qdd, 1e-7, f"tiled fd round trip B={B}")
+        with pytest.raises(ValueError):
+            mb.rnea_batch_tiled(xt[0][:, :, :128].contiguous(), xt[1], xt[2], 65536 + 3)
+    finally:
+        ffi.set_tuning("jit", 1)

@@ -39,5 +39,9 @@ def run(rows_in, rows_out, width, nt=0, B=1 << 20, steps=100, rounds=5):
 
 
 if __name__ == "__main__":
-    out = [run(ri, ro, w, nt) for ri, ro in ((21, 7), (90, 30), (4, 4)) for w in (1, 4) for nt in (0, 1, 2, 3)]
+    if len(sys.argv) > 1 and sys.argv[1] == "tiled":
+        # SoA rows vs the tiled layout (nt bit 2), 4 B lanes, RNEA 7-DOF shape, three batch sizes
+        out = [run(21, 7, 1, nt, B=B) for B in (1 << 20, 1 << 21, 1 << 22) for nt in (0, 3, 4, 7)]
+    else:
+        out = [run(ri, ro, w, nt) for ri, ro in ((21, 7), (90, 30), (4, 4)) for w in (1, 4) for nt in (0, 1, 2, 3)]
     print(json.dumps(out, indent=1))
