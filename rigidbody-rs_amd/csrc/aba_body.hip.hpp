@@ -127,13 +127,73 @@ __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, 
                                          int64_t ld) {
     const uint32_t off = b * (uint32_t)sizeof(T);
     T qv[N], qdv[N], tv[N];
+    // In order of first use: q, qd root->leaf (pass 1), tau leaf->root (pass 2).  A
+    // scheduling barrier after each load pins this issue order; loads retire in issue order,
+    // so every counted wait releases as soon as its own row has arrived, and all loads are in
+    // flight before the first wait.
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         qv[j] = ld_row(q, j * ld, off);
+        __builtin_amdgcn_sched_barrier(0);
         qdv[j] = ld_row(qd, j * ld, off);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) {
         tv[j] = ld_row(tau, j * ld, off);
+        __builtin_amdgcn_sched_barrier(0);
     }
     aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
+}
+
+// Resident grid-stride form (A/B, model-specialised kernels): each lane walks the batch
+// with stride gridDim.x * 256 and issues the NEXT configuration's q, qd loads before
+// evaluating the current one (14 VGPRs in fp32 FR3); tau is loaded per configuration, its
+// latency hidden behind pass 1.  Block k of pass i covers configurations
+// (k + i * gridDim.x) * 256 + [0, 256); the tiled / SoA block base is o(b0) =
+// (b0 / 256) * bs + b0 % 256 as in the lane kernels.
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void aba_stream(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                           const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
+                                           int64_t ld, int64_t bs) {
+    const uint32_t off = threadIdx.x * (uint32_t)sizeof(T);
+    uint32_t blk = blockIdx.x;
+    const uint32_t nblk = (B + 255u) / 256u;
+    auto base = [&](uint32_t k) { return (int64_t)k * bs; };
+    T qv[N], qdv[N];
+    bool live = blk * 256u + threadIdx.x < B;
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q + base(blk), j * ld, off);
+            qdv[j] = ld_row(qd + base(blk), j * ld, off);
+        }
+    }
+    while (blk < nblk) {
+        const uint32_t nxt = blk + gridDim.x;
+        const bool nlive = nxt < nblk && nxt * 256u + threadIdx.x < B;
+        T nq[N], nqd[N], tv[N];
+        if (nlive) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                nq[j] = ld_row(q + base(nxt), j * ld, off);
+                nqd[j] = ld_row(qd + base(nxt), j * ld, off);
+            }
+        }
+        if (live) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) tv[j] = ld_row(tau + base(blk), j * ld, off);
+            T *out = qdd + base(blk);
+            aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(out, j * ld, off, v); });
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = nq[j];
+            qdv[j] = nqd[j];
+        }
+        live = nlive;
+        blk = nxt;
+    }
 }
 
 // Fused rollout (the MPC-shooting use of forward dynamics): K steps

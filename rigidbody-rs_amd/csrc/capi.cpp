@@ -130,7 +130,8 @@ int device_consts(const Multibody *mb, const T **out) {
 
 // Resident grid-stride form of a JIT kernel (tuning.hpp policies).
 bool jit_stream(rbamd::JitKind kind, bool f64, int n) {
-    return kind == rbamd::JitKind::Rnea && rbamd::rnea_use_stream(f64, n, true);
+    return (kind == rbamd::JitKind::Rnea && rbamd::rnea_use_stream(f64, n, true)) ||
+           (kind == rbamd::JitKind::Fd && rbamd::tuning().fd_stream > 0);
 }
 
 // The hipRTC kernel of `kind` for this model on the current device, or nullptr (the
@@ -702,6 +703,7 @@ int rb_set_tuning(const char *key, int value) {
     else if (k == "jit_waves") t.jit_waves = value;
     else if (k == "jit_variant") t.jit_variant = value;
     else if (k == "opaque_consts") t.opaque_consts = value;
+    else if (k == "fd_stream") t.fd_stream = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

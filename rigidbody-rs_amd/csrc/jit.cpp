@@ -123,10 +123,14 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
-        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
-        o << "  if (b >= B) return;\n";
-        o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
-        o << "  rbamd::dev::aba_lane<T, N, " << F << ">(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
+        if (stream) {
+            o << "  rbamd::dev::aba_stream<T, N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
+        } else {
+            o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+            o << "  if (b >= B) return;\n";
+            o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+            o << "  rbamd::dev::aba_lane<T, N, " << F << ">(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
+        }
     } else if (kind == JitKind::Rollout) {
         o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
              "int K, T *__restrict__ traj, uint32_t B, int64_t ld) {\n";

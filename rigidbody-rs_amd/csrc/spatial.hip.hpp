@@ -221,19 +221,44 @@ __device__ __forceinline__ void inertia_mul(const Link<T> &L, const V3<T> &w, co
 #ifndef RB_NT
 #define RB_NT 0
 #endif
+// Row pointers are typed global (address_space(1)): from a generic pointer the compiler
+// strength-reduces consecutive row addresses into chained 64-bit per-lane VGPR adds (68 of
+// them in the FR3 RNEA kernel), which costs VALU and VGPRs and -- when it reuses a pending
+// load's destination register as an address half -- a full memory-latency wait in the middle
+// of the load burst.  Typed global, every access is the saddr form: uniform 64-bit row base
+// in SGPRs + the lane's 32-bit byte offset.  (RB_VARIANT bit 6 restores the generic form
+// for A/B measurements.)
+template <typename T>
+using gptr = __attribute__((address_space(1))) T *;
+
 template <typename T>
 __device__ __forceinline__ T ld_row(const T *__restrict__ base, int64_t row, uint32_t off) {
-    const T *p = reinterpret_cast<const T *>(reinterpret_cast<const char *>(base + row) + off);
-    if constexpr ((RB_NT & 1) != 0) return __builtin_nontemporal_load(p);
-    return *p;
+    if constexpr ((RB_VARIANT & 64) != 0) {
+        const T *p = reinterpret_cast<const T *>(reinterpret_cast<const char *>(base + row) + off);
+        if constexpr ((RB_NT & 1) != 0) return __builtin_nontemporal_load(p);
+        return *p;
+    } else {
+        gptr<const T> p = (gptr<const T>)((gptr<const char>)(base + row) + off);
+        if constexpr ((RB_NT & 1) != 0) return __builtin_nontemporal_load(p);
+        return *p;
+    }
 }
 template <typename T>
 __device__ __forceinline__ void st_row(T *__restrict__ base, int64_t row, uint32_t off, T v) {
-    T *p = reinterpret_cast<T *>(reinterpret_cast<char *>(base + row) + off);
-    if constexpr ((RB_NT & 2) != 0) {
-        __builtin_nontemporal_store(v, p);
+    if constexpr ((RB_VARIANT & 64) != 0) {
+        T *p = reinterpret_cast<T *>(reinterpret_cast<char *>(base + row) + off);
+        if constexpr ((RB_NT & 2) != 0) {
+            __builtin_nontemporal_store(v, p);
+        } else {
+            *p = v;
+        }
     } else {
-        *p = v;
+        gptr<T> p = (gptr<T>)((gptr<char>)(base + row) + off);
+        if constexpr ((RB_NT & 2) != 0) {
+            __builtin_nontemporal_store(v, p);
+        } else {
+            *p = v;
+        }
     }
 }
 

@@ -27,6 +27,7 @@ Tuning &tuning() {
         x.rnea_nt = env_int("RB_RNEA_NT", x.rnea_nt);
         x.fd_nt = env_int("RB_FD_NT", x.fd_nt);
         x.opaque_consts = env_int("RB_OPAQUE_CONSTS", x.opaque_consts);
+        x.fd_stream = env_int("RB_FD_STREAM", x.fd_stream);
         x.jit_waves = env_int("RB_JIT_WAVES", x.jit_waves);
         x.jit_variant = env_int("RB_JIT_VARIANT", x.jit_variant);
         return x;

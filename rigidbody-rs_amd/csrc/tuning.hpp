@@ -28,6 +28,8 @@ struct Tuning {
     // 35.7 us) of chains up to 16 links; off for fp64 forward dynamics (90 vs 71 us), for
     // longer chains (30-link fp32 FD: 1331 vs 333 us) and for the other kinds.
     int opaque_consts = -1;
+    // JIT forward dynamics: 1 = resident grid-stride form with register prefetch (aba_stream).
+    int fd_stream = 0;
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
     int jit_variant = 0;
 };
