@@ -18,7 +18,9 @@ Like the reference it injects joint motion about local z (multibody.rs:130-138)
 and applies gravity as a +9.81 z base acceleration (multibody.rs:117-120).  With
 general=True the motion subspace is the joint's own axis, S_i = [axis_i; 0] -- the
 general-axis extension the reference does not have; this module
-is then its only independent check.
+is then its only independent check.  Likewise for kinematic trees (frames["parent"]) and
+prismatic joints (frames["prismatic"], S_i = [0; axis_i]): Featherstone's tree forms of
+Tables 5.1 / 6.2 / 7.1 with the parent array lambda(i) < i.
 """
 from __future__ import annotations
 
@@ -89,6 +91,8 @@ class Model6:
             self.axis = [np.asarray(frames["axis"][i], float) for i in range(self.n)]
             self.I = [inertia6(frames["mass"][i], np.asarray(frames["com"][i], float),
                                np.asarray(frames["icom"][i], float)) for i in range(self.n)]
+            self.parent = [int(x) for x in frames.get("parent", np.arange(self.n) - 1)]
+            self.prismatic = [bool(x) for x in frames.get("prismatic", np.zeros(self.n))]
         else:
             self.n = int(raw["n"])
             self.Rp = [rpy_matrix(*raw["rpy"][i]) for i in range(self.n)]
@@ -99,47 +103,65 @@ class Model6:
                 j = raw["inertia6"][i]
                 ic = np.array([[j[0], j[1], j[2]], [j[1], j[3], j[4]], [j[2], j[4], j[5]]])
                 self.I.append(inertia6(raw["mass"][i], np.asarray(raw["com"][i], float), ic))
+            self.parent = list(range(-1, self.n - 1))
+            self.prismatic = [False] * self.n
         self.S = []
         for i in range(self.n):
             a = self.axis[i] / np.linalg.norm(self.axis[i]) if general else np.array([0.0, 0.0, 1.0])
-            self.S.append(np.concatenate([a, np.zeros(3)]))
+            self.S.append(np.concatenate([np.zeros(3), a] if self.prismatic[i] else [a, np.zeros(3)]))
 
     def poses(self, q):
-        return [(self.Rp[i] @ axis_angle_matrix(self.axis[i], q[i]), self.p[i]) for i in range(self.n)]
+        out = []
+        for i in range(self.n):
+            if self.prismatic[i]:
+                a = self.axis[i] / np.linalg.norm(self.axis[i])
+                out.append((self.Rp[i], self.p[i] + self.Rp[i] @ (a * q[i])))
+            else:
+                out.append((self.Rp[i] @ axis_angle_matrix(self.axis[i], q[i]), self.p[i]))
+        return out
+
+    def ancestors(self, i):
+        """i, parent(i), ..., root."""
+        out = []
+        while i >= 0:
+            out.append(i)
+            i = self.parent[i]
+        return out
 
     def xforms(self, q):
         return [xmotion(R.T, p) for R, p in self.poses(q)]
 
     def rnea(self, q, qd, qdd):
         X = self.xforms(q)
-        v = np.zeros(6)
-        a = np.array([0, 0, 0, 0, 0, G], float)
-        f = []
+        v0, a0 = np.zeros(6), np.array([0, 0, 0, 0, 0, G], float)
+        v, a, f = [None] * self.n, [None] * self.n, []
         for i in range(self.n):
+            p = self.parent[i]
             vJ = self.S[i] * qd[i]
-            v = X[i] @ v + vJ
-            a = X[i] @ a + self.S[i] * qdd[i] + crm(v) @ vJ
-            f.append(self.I[i] @ a + crf(v) @ self.I[i] @ v)
+            v[i] = X[i] @ (v0 if p < 0 else v[p]) + vJ
+            a[i] = X[i] @ (a0 if p < 0 else a[p]) + self.S[i] * qdd[i] + crm(v[i]) @ vJ
+            f.append(self.I[i] @ a[i] + crf(v[i]) @ self.I[i] @ v[i])
         tau = np.zeros(self.n)
         for i in range(self.n - 1, -1, -1):
             tau[i] = self.S[i] @ f[i]
-            if i > 0:
-                f[i - 1] = f[i - 1] + X[i].T @ f[i]
+            if self.parent[i] >= 0:
+                f[self.parent[i]] = f[self.parent[i]] + X[i].T @ f[i]
         return tau
 
     def crba(self, q):
         X = self.xforms(q)
         Ic = [M.copy() for M in self.I]
-        for i in range(self.n - 1, 0, -1):
-            Ic[i - 1] = Ic[i - 1] + X[i].T @ Ic[i] @ X[i]
+        for i in range(self.n - 1, -1, -1):
+            if self.parent[i] >= 0:
+                Ic[self.parent[i]] = Ic[self.parent[i]] + X[i].T @ Ic[i] @ X[i]
         H = np.zeros((self.n, self.n))
         for i in range(self.n):
             F = Ic[i] @ self.S[i]
             H[i, i] = self.S[i] @ F
             j = i
-            while j > 0:
+            while self.parent[j] >= 0:
                 F = X[j].T @ F
-                j -= 1
+                j = self.parent[j]
                 H[i, j] = H[j, i] = self.S[j] @ F
         return H
 
@@ -147,47 +169,49 @@ class Model6:
         n = self.n
         X = self.xforms(q)
         v, c, IA, pA = [None] * n, [None] * n, [None] * n, [None] * n
-        vp = np.zeros(6)
         for i in range(n):
             vJ = self.S[i] * qd[i]
-            v[i] = X[i] @ vp + vJ
+            v[i] = X[i] @ (np.zeros(6) if self.parent[i] < 0 else v[self.parent[i]]) + vJ
             c[i] = crm(v[i]) @ vJ
             IA[i] = self.I[i].copy()
             pA[i] = crf(v[i]) @ self.I[i] @ v[i]
-            vp = v[i]
         U, D, u = [None] * n, np.zeros(n), np.zeros(n)
         for i in range(n - 1, -1, -1):
             U[i] = IA[i] @ self.S[i]
             D[i] = self.S[i] @ U[i]
             u[i] = tau[i] - self.S[i] @ pA[i]
-            if i > 0:
+            p = self.parent[i]
+            if p >= 0:
                 Ia = IA[i] - np.outer(U[i], U[i]) / D[i]
                 pa = pA[i] + Ia @ c[i] + U[i] * u[i] / D[i]
-                IA[i - 1] = IA[i - 1] + X[i].T @ Ia @ X[i]
-                pA[i - 1] = pA[i - 1] + X[i].T @ pa
+                IA[p] = IA[p] + X[i].T @ Ia @ X[i]
+                pA[p] = pA[p] + X[i].T @ pa
         qdd = np.zeros(n)
-        ap = np.array([0, 0, 0, 0, 0, G], float)
+        a = [None] * n
         for i in range(n):
-            a = X[i] @ ap + c[i]
-            qdd[i] = (u[i] - U[i] @ a) / D[i]
-            a = a + self.S[i] * qdd[i]
-            ap = a
+            p = self.parent[i]
+            a[i] = X[i] @ (np.array([0, 0, 0, 0, 0, G], float) if p < 0 else a[p]) + c[i]
+            qdd[i] = (u[i] - U[i] @ a[i]) / D[i]
+            a[i] = a[i] + self.S[i] * qdd[i]
         return qdd
 
     def fwd_kin(self, q):
         R, p = np.eye(3), np.zeros(3)
-        for Ri, pi in self.poses(q):
+        poses = self.poses(q)
+        for i in reversed(self.ancestors(self.n - 1)):  # root -> last link
+            Ri, pi = poses[i]
             p = p + R @ pi
             R = R @ Ri
         return p
 
     def jac(self, q):
-        """Body Jacobian of the last link, rows [lin; rot] (multibody.rs:95-108)."""
+        """Body Jacobian of the last link, rows [lin; rot] (multibody.rs:95-108); columns of
+        joints off its path to the root are zero."""
         poses = self.poses(q)
         n = self.n
         J = np.zeros((6, n))
         R, p = np.eye(3), np.zeros(3)  # pose of the last frame in frame i (built backwards)
-        for i in range(n - 1, -1, -1):
+        for i in self.ancestors(n - 1):
             # joint-i axis z in frame i, expressed at/in the last frame: X(R^T, p) applied to S
             X = xmotion(R.T, p)
             sv = X @ self.S[i]

@@ -342,6 +342,7 @@ int oracle_model_from_raw(oracle_model *m, int n,
         memcpy(m->com[i], I.com, sizeof I.com);
         memcpy(m->icom[i], I.icom, sizeof I.icom);
         memcpy(m->io[i], I.io, sizeof I.io);
+        m->parent[i] = i - 1;
     }
     return 0;
 }
@@ -387,11 +388,24 @@ int oracle_model_from_frames(oracle_model *m, int n, const double *Rp, const dou
         memcpy(m->com[i], I.com, sizeof I.com);
         memcpy(m->icom[i], I.icom, sizeof I.icom);
         memcpy(m->io[i], I.io, sizeof I.io);
+        m->parent[i] = i - 1;
     }
     return 0;
 }
 
 void oracle_model_set_general_axes(oracle_model *m, int on) { m->general_axes = on != 0; }
+
+int oracle_model_set_topology(oracle_model *m, const int *parent, const int *prismatic) {
+    for (int i = 0; i < m->n; ++i) {
+        if (parent && (parent[i] < -1 || parent[i] >= i)) return -1;
+        if (prismatic && prismatic[i] != 0 && prismatic[i] != 1) return -1;
+    }
+    for (int i = 0; i < m->n; ++i) {
+        if (parent) m->parent[i] = parent[i];
+        if (prismatic) m->prismatic[i] = prismatic[i];
+    }
+    return 0;
+}
 
 /* Motion subspace of joint i: the reference's z (spatial.rs:180-185) or the true axis. */
 static void joint_axis(const oracle_model *m, int i, double s[3]) {
@@ -407,6 +421,14 @@ static iso3 parent_to_child(const oracle_model *m, int i, double qi) {
     iso3 r;
     double sa[3] = {m->axis[i][0] * qi, m->axis[i][1] * qi, m->axis[i][2] * qi};
     double jq[4];
+    if (m->prismatic[i]) {
+        /* prismatic: the joint origin, then a translation by axis * q in the joint frame */
+        double d[3];
+        oracle_quat_rotate(m->pq[i], sa, d);
+        memcpy(r.q, m->pq[i], sizeof r.q);
+        for (int k = 0; k < 3; ++k) r.t[k] = m->pt[i][k] + d[k];
+        return r;
+    }
     oracle_quat_from_scaled_axis(sa, jq);
     qmul(m->pq[i], jq, r.q);
     memcpy(r.t, m->pt[i], sizeof r.t);
@@ -428,13 +450,22 @@ static void get_transforms(const oracle_model *m, const double *q, iso3 *tr) {
 /* Multibody::rnea, multibody.rs:111-153 */
 static void rnea_tr(const oracle_model *m, const iso3 *tr, const double *dq,
                     const double *ddq, double *tau) {
-    sv6 f[ORACLE_MAX_DOF];
-    sv6 v = {{0, 0, 0}, {0, 0, 0}};
-    sv6 a = {{0, 0, GRAVITY}, {0, 0, 0}};
+    sv6 f[ORACLE_MAX_DOF], V[ORACLE_MAX_DOF], A[ORACLE_MAX_DOF];
+    const sv6 v0 = {{0, 0, 0}, {0, 0, 0}};
+    const sv6 a0 = {{0, 0, GRAVITY}, {0, 0, 0}};
     for (int i = 0; i < m->n; ++i) {
-        v = motion_tf(&tr[i], &v);
-        a = motion_tf(&tr[i], &a);
-        if (!m->general_axes) {
+        const int p = m->parent[i]; /* serial chain: i - 1 */
+        sv6 v = motion_tf(&tr[i], p < 0 ? &v0 : &V[p]);
+        sv6 a = motion_tf(&tr[i], p < 0 ? &a0 : &A[p]);
+        if (m->prismatic[i]) {
+            /* v += S qd; a += S qdd + v x (S qd), S = (rot 0, lin s) */
+            double s[3], c[3];
+            joint_axis(m, i, s);
+            for (int k = 0; k < 3; ++k) v.lin[k] += s[k] * dq[i];
+            for (int k = 0; k < 3; ++k) a.lin[k] += s[k] * ddq[i];
+            cross3(v.rot, s, c);
+            for (int k = 0; k < 3; ++k) a.lin[k] += c[k] * dq[i];
+        } else if (!m->general_axes) {
             /* multibody.rs:126-138, z hard-coded */
             v.rot[2] += dq[i];
             a.rot[2] += ddq[i];
@@ -453,6 +484,8 @@ static void rnea_tr(const oracle_model *m, const iso3 *tr, const double *dq,
             cross3(v.rot, s, c);
             for (int k = 0; k < 3; ++k) a.rot[k] += c[k] * dq[i];
         }
+        V[i] = v;
+        A[i] = a;
         inertia_t I = body_of(m, i);
         sv6 Ia = inertia_mul(&I, &a);
         sv6 Iv = inertia_mul(&I, &v);
@@ -465,14 +498,18 @@ static void rnea_tr(const oracle_model *m, const iso3 *tr, const double *dq,
     for (int i = m->n - 1; i >= 0; --i) {
         double s[3];
         joint_axis(m, i, s);
-        tau[i] = m->general_axes ? s[0] * f[i].rot[0] + s[1] * f[i].rot[1] + s[2] * f[i].rot[2] : f[i].rot[2];
-        if (i > 0) {
+        if (m->prismatic[i])
+            tau[i] = s[0] * f[i].lin[0] + s[1] * f[i].lin[1] + s[2] * f[i].lin[2];
+        else
+            tau[i] = m->general_axes ? s[0] * f[i].rot[0] + s[1] * f[i].rot[1] + s[2] * f[i].rot[2] : f[i].rot[2];
+        const int p = m->parent[i];
+        if (p >= 0) {
             iso3 inv;
             iso_inv(&tr[i], &inv);
             sv6 ft = force_tf(&inv, &f[i]);
             for (int k = 0; k < 3; ++k) {
-                f[i - 1].lin[k] += ft.lin[k];
-                f[i - 1].rot[k] += ft.rot[k];
+                f[p].lin[k] += ft.lin[k];
+                f[p].rot[k] += ft.rot[k];
             }
         }
     }
@@ -493,11 +530,18 @@ void oracle_crba(const oracle_model *m, const double *q, double *H) {
     get_transforms(m, q, tr);
     for (int c = 0; c < n; ++c)
         for (int r = 0; r < n; ++r) H[r + n * c] = (r == c) ? 1.0 : 0.0;
-    inertia_t I = body_of(m, n - 1);
+    /* composite inertias; in a tree a parent's entry accumulates each child's (for the
+     * serial chain this is exactly body(i-1) + moved, multibody.rs:170) */
+    inertia_t Ic[ORACLE_MAX_DOF];
+    for (int i = 0; i < n; ++i) Ic[i] = body_of(m, i);
     for (int i = n - 1; i >= 0; --i) {
+        const inertia_t I = Ic[i];
         sv6 S = {{0, 0, 0}, {0, 0, 0}}; /* BodyJacobian::revolute_z, spatial.rs:180-185 */
-        joint_axis(m, i, S.rot);
-        if (!m->general_axes) {
+        joint_axis(m, i, m->prismatic[i] ? S.lin : S.rot);
+        if (m->prismatic[i]) {
+            sv6 F0 = inertia_mul(&I, &S);
+            H[i + n * i] = S.lin[0] * F0.lin[0] + S.lin[1] * F0.lin[1] + S.lin[2] * F0.lin[2];
+        } else if (!m->general_axes) {
             H[i + n * i] = I.io[8]; /* get_rotz, inertia.rs:91-93 */
         } else {
             double Is[3];
@@ -505,18 +549,23 @@ void oracle_crba(const oracle_model *m, const double *q, double *H) {
             H[i + n * i] = S.rot[0] * Is[0] + S.rot[1] * Is[1] + S.rot[2] * Is[2];
         }
         sv6 F = inertia_mul(&I, &S);
-        for (int j = i - 1; j >= 0; --j) {
+        /* carry F to every ancestor j of i (serial: j = i-1 .. 0, multibody.rs:163-168) */
+        for (int c = i, j = m->parent[i]; j >= 0; c = j, j = m->parent[j]) {
             iso3 inv;
-            iso_inv(&tr[j + 1], &inv);
+            iso_inv(&tr[c], &inv);
             F = force_tf(&inv, &F);
             double sj[3];
             joint_axis(m, j, sj);
-            H[j + n * i] = m->general_axes ? sj[0] * F.rot[0] + sj[1] * F.rot[1] + sj[2] * F.rot[2] : F.rot[2];
+            if (m->prismatic[j])
+                H[j + n * i] = sj[0] * F.lin[0] + sj[1] * F.lin[1] + sj[2] * F.lin[2];
+            else
+                H[j + n * i] = m->general_axes ? sj[0] * F.rot[0] + sj[1] * F.rot[1] + sj[2] * F.rot[2] : F.rot[2];
         }
-        if (i > 0) {
+        const int p = m->parent[i];
+        if (p >= 0) {
             inertia_t moved = inertia_transform(&I, &tr[i]);
-            inertia_t parent = body_of(m, i - 1);
-            I = inertia_add(&parent, &moved);
+            inertia_t parent = Ic[p];
+            Ic[p] = inertia_add(&parent, &moved);
         }
     }
 }
@@ -526,7 +575,8 @@ void oracle_fwd_kin(const oracle_model *m, const double *q, double *pos) {
     iso3 tr[ORACLE_MAX_DOF];
     get_transforms(m, q, tr);
     iso3 acc = {{0, 0, 0, 1}, {0, 0, 0}};
-    for (int i = m->n - 1; i >= 0; --i) {
+    /* the last link's ancestors, leaf to root (serial: n-1 .. 0) */
+    for (int i = m->n - 1; i >= 0; i = m->parent[i]) {
         iso3 nxt;
         iso_mul(&tr[i], &acc, &nxt);
         acc = nxt;
@@ -539,9 +589,10 @@ void oracle_jac(const oracle_model *m, const double *q, double *J) {
     iso3 tr[ORACLE_MAX_DOF];
     get_transforms(m, q, tr);
     iso3 acc = {{0, 0, 0, 1}, {0, 0, 0}};
-    for (int i = m->n - 1; i >= 0; --i) {
+    memset(J, 0, 6 * (size_t)m->n * sizeof(double)); /* joints off the last link's path */
+    for (int i = m->n - 1; i >= 0; i = m->parent[i]) {
         sv6 S = {{0, 0, 0}, {0, 0, 0}};
-        joint_axis(m, i, S.rot);
+        joint_axis(m, i, m->prismatic[i] ? S.lin : S.rot);
         sv6 v = motion_tf(&acc, &S);
         for (int k = 0; k < 3; ++k) {
             J[6 * i + k] = v.lin[k];

@@ -44,6 +44,13 @@ typedef struct {
      *    axes is pinned by the independent 6x6 formulation (featherstone6.py), not the
      *    reference (which has no consistent general-axis dynamics). */
     int general_axes;
+    /* Kinematic tree (beyond the reference's serial chain): parent
+     * link index (-1 = the fixed base; parent[i] < i, so index order is a topological
+     * order) and joint type (0 revolute, 1 prismatic along `axis`).  Every constructor
+     * sets the reference's serial revolute chain (parent[i] = i - 1); the algorithms then
+     * perform exactly the operations of the serial code path. */
+    int parent[ORACLE_MAX_DOF];
+    int prismatic[ORACLE_MAX_DOF];
 } oracle_model;
 
 /* Raw per-revolute-joint URDF values, 16 doubles per joint:
@@ -60,6 +67,9 @@ int oracle_model_from_frames(oracle_model *m, int n, const double *Rp, const dou
                              const double *axis, const double *mass, const double *com,
                              const double *icom9);
 void oracle_model_set_general_axes(oracle_model *m, int on);
+/* Tree topology and joint types (parent[i] in [-1, i), prismatic[i] in {0, 1}); NULL keeps
+ * the current array.  Returns 0, or -1 on a bad parent / type. */
+int oracle_model_set_topology(oracle_model *m, const int *parent, const int *prismatic);
 
 int oracle_model_dof(const oracle_model *m);
 int oracle_model_size(void);

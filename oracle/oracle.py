@@ -51,6 +51,9 @@ def lib():
         L.oracle_model_from_frames.restype = ctypes.c_int
         L.oracle_model_from_frames.argtypes = [ctypes.c_void_p, ctypes.c_int] + [_dp] * 6
         L.oracle_model_set_general_axes.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _ip = ctypes.POINTER(ctypes.c_int)
+        L.oracle_model_set_topology.restype = ctypes.c_int
+        L.oracle_model_set_topology.argtypes = [ctypes.c_void_p, _ip, _ip]
         L.oracle_quat_from_scaled_axis.argtypes = [_dp, _dp]
         L.oracle_quat_from_axis_angle.argtypes = [_dp, ctypes.c_double, _dp]
         L.oracle_quat_to_matrix.argtypes = [_dp, _dp]
@@ -78,7 +81,8 @@ class Model:
     """fp64 oracle model built from raw URDF values (oracle/urdf_model.py).
 
     general=True: motion subspace along each joint's own axis (oracle.h general_axes);
-    frames=...: the tree-mode reading (urdf_model.model_frames_from_urdf_tree)."""
+    frames=...: the tree-mode reading (urdf_model.model_frames_from_urdf_tree), whose
+    optional "parent" / "prismatic" entries give a kinematic tree and joint types."""
 
     def __init__(self, raw=None, general=False, frames=None):
         L = lib()
@@ -96,6 +100,15 @@ class Model:
         if rc != 0:
             raise ValueError(f"oracle model construction failed: {rc}")
         L.oracle_model_set_general_axes(self._buf, int(bool(general)))
+        if frames is not None and ("parent" in frames or "prismatic" in frames):
+            par = np.ascontiguousarray(frames.get("parent", np.arange(self.n) - 1), dtype=np.int32)
+            pri = np.ascontiguousarray(frames.get("prismatic", np.zeros(self.n)), dtype=np.int32)
+            self._keep += [par, pri]
+            _ip = ctypes.POINTER(ctypes.c_int)
+            if L.oracle_model_set_topology(self._buf, par.ctypes.data_as(_ip), pri.ctypes.data_as(_ip)) != 0:
+                raise ValueError("bad tree topology")
+        self.parent = (np.asarray(frames["parent"], int) if frames is not None and "parent" in frames
+                       else np.arange(self.n) - 1)
 
     @property
     def ptr(self):

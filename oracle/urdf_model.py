@@ -121,21 +121,35 @@ def _skew(v):
     return np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
 
 
-def model_frames_from_urdf_tree(xml_text: str):
-    """Serial chain by joint parent/child names from the root link; fixed joints merged.
-    Returns dict(Rp [n,3,3], p [n,3], axis [n,3] (unit), mass [n], com [n,3], icom [n,3,3],
-    limits [n]) -- body i is joint i's child link plus its fixed-joint subtree."""
+# Floating base (RB_MODEL_FLOATING_BASE): six massless virtual joints from the world to the
+# root body -- prismatic x, y, z (world axes), then revolute z, y, x (yaw, pitch, roll: the
+# root orientation is Rz Ry Rx, singular at pitch = +-pi/2).  Their "limits" only shape
+# test / benchmark inputs (pitch kept within +-1.2 rad).
+FLOAT_AXES = ((1.0, 0.0, 0.0), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (1.0, 0.0, 0.0))
+FLOAT_PRISMATIC = (1, 1, 1, 0, 0, 0)
+FLOAT_LIMITS = tuple({"lower": lo, "upper": hi, "velocity": v, "effort": 1000.0}
+                     for lo, hi, v in ((-1.0, 1.0, 1.0),) * 3 + ((-np.pi, np.pi, 2.0), (-1.2, 1.2, 2.0), (-np.pi, np.pi, 2.0)))
+MOVABLE = ("revolute", "continuous", "prismatic")
+
+
+def model_frames_from_urdf_tree(xml_text: str, floating: bool = False):
+    """Kinematic tree by joint parent/child names from the root link; fixed joints merged.
+    Links are numbered in depth-first preorder (a body's movable child joints in the order
+    a stack walk of its fixed subtree meets them, each link's joints in document order), so
+    parent[i] < i.  Returns dict(Rp [n,3,3], p [n,3], axis [n,3] (unit), mass [n],
+    com [n,3], icom [n,3,3], parent [n], prismatic [n], limits [n]) -- body i is joint i's
+    child link plus its fixed-joint subtree.  floating=True prepends the six virtual
+    joints above and gives the root body to the last of them."""
     links, joints = parse_robot(xml_text)
     by_name = {l["name"]: l for l in links}
     children = [j["child"] for j in joints]
     roots = [l["name"] for l in links if l["name"] not in children]
     if len(roots) != 1:
         raise ValueError(f"expected one root link, got {roots}")
-    out = {k: [] for k in ("Rp", "p", "axis", "mass", "com", "icom", "limits")}
-    cur, base = roots[0], True
-    while True:
-        parts, nxt = [], None  # (link, R, t) of the body's fixed subtree
-        stack = [(cur, np.eye(3), np.zeros(3))]
+
+    def body(root_link):
+        parts, movable = [], []  # (link, R, t) of the body's fixed subtree; its movable joints
+        stack = [(root_link, np.eye(3), np.zeros(3))]
         while stack:
             ln, R, t = stack.pop()
             parts.append((by_name[ln], R, t))
@@ -147,36 +161,58 @@ def model_frames_from_urdf_tree(xml_text: str):
                 Rj, tj = R @ _rpy(*j["rpy"]), t + R @ np.asarray(j["xyz"], float)
                 if j["type"] == "fixed":
                     stack.append((j["child"], Rj, tj))
-                elif j["type"] in ("revolute", "continuous"):
-                    if nxt is not None:
-                        raise ValueError("branching tree")
-                    nxt = (j, Rj, tj)
+                elif j["type"] in MOVABLE:
+                    movable.append((j, Rj, tj))
                 else:
                     raise ValueError(f"joint type {j['type']}")
-        if not base:
-            m = sum(l["mass"] for l, _, _ in parts)
-            c = sum(l["mass"] * (R @ np.asarray(l["com"], float) + t) for l, R, t in parts)
-            c = c / m if m > 0 else np.zeros(3)
-            Ic = np.zeros((3, 3))
-            for l, R, t in parts:
-                i6 = l["inertia6"]
-                Il = np.array([[i6[0], i6[1], i6[2]], [i6[1], i6[3], i6[4]], [i6[2], i6[4], i6[5]]])
-                Rin = R @ _rpy(*l["com_rpy"])
-                d = R @ np.asarray(l["com"], float) + t - c
-                Ic += Rin @ Il @ Rin.T + l["mass"] * (d @ d * np.eye(3) - np.outer(d, d))
-            out["mass"].append(m)
-            out["com"].append(c)
-            out["icom"].append(Ic)
-        if nxt is None:
-            break
-        j, Rj, tj = nxt
-        a = np.asarray(j["axis"], float)
-        out["Rp"].append(Rj)
-        out["p"].append(tj)
+        m = sum(l["mass"] for l, _, _ in parts)
+        c = sum(l["mass"] * (R @ np.asarray(l["com"], float) + t) for l, R, t in parts)
+        c = c / m if m > 0 else np.zeros(3)
+        Ic = np.zeros((3, 3))
+        for l, R, t in parts:
+            i6 = l["inertia6"]
+            Il = np.array([[i6[0], i6[1], i6[2]], [i6[1], i6[3], i6[4]], [i6[2], i6[4], i6[5]]])
+            Rin = R @ _rpy(*l["com_rpy"])
+            d = R @ np.asarray(l["com"], float) + t - c
+            Ic += Rin @ Il @ Rin.T + l["mass"] * (d @ d * np.eye(3) - np.outer(d, d))
+        return (m, c, Ic), movable
+
+    out = {k: [] for k in ("Rp", "p", "axis", "parent", "prismatic", "limits")}
+    bodies = {}
+
+    def add_link(R, t, axis, prismatic, parent, limits):
+        a = np.asarray(axis, float)
+        out["Rp"].append(R)
+        out["p"].append(t)
         out["axis"].append(a / np.linalg.norm(a))
-        out["limits"].append(j["limit"])
-        cur, base = j["child"], False
-    res = {k: np.array(v, dtype=np.float64) for k, v in out.items() if k != "limits"}
+        out["parent"].append(parent)
+        out["prismatic"].append(int(prismatic))
+        out["limits"].append(limits)
+        return len(out["Rp"]) - 1
+
+    def visit(j, Rj, tj, parent):
+        i = add_link(Rj, tj, j["axis"], j["type"] == "prismatic", parent, j["limit"])
+        bodies[i], movable = body(j["child"])
+        for jc, Rc, tc in movable:
+            visit(jc, Rc, tc, i)
+
+    root_body, movable = body(roots[0])
+    base = -1
+    if floating:
+        for k in range(6):
+            add_link(np.eye(3), np.zeros(3), FLOAT_AXES[k], FLOAT_PRISMATIC[k], k - 1, dict(FLOAT_LIMITS[k]))
+            bodies[k] = (0.0, np.zeros(3), np.zeros((3, 3)))
+        bodies[5] = root_body
+        base = 5
+    for j, Rj, tj in movable:
+        visit(j, Rj, tj, base)
+    n = len(out["Rp"])
+    res = {k: np.array(out[k], dtype=np.float64) for k in ("Rp", "p", "axis")}
+    res["parent"] = np.array(out["parent"], dtype=np.int32)
+    res["prismatic"] = np.array(out["prismatic"], dtype=np.int32)
+    res["mass"] = np.array([bodies[i][0] for i in range(n)], dtype=np.float64)
+    res["com"] = np.array([bodies[i][1] for i in range(n)], dtype=np.float64).reshape(n, 3)
+    res["icom"] = np.array([bodies[i][2] for i in range(n)], dtype=np.float64).reshape(n, 3, 3)
     res["limits"] = out["limits"]
-    res["n"] = len(out["mass"])
+    res["n"] = n
     return res

@@ -139,6 +139,81 @@ def general_chain_urdf(n: int, seed: int = 7) -> str:
             + "\n".join(joints[i] for i in order) + "\n</robot>\n").replace("{n}", str(n))
 
 
+def tree_urdf(seed: int = 11, floating: bool = False) -> str:
+    """Branching test model (RB_MODEL_URDF_TREE | RB_MODEL_GENERAL_AXES):
+    a prismatic lift base -> torso, then three branches off the torso body -- a 3-joint arm
+    (revolute, revolute, continuous), a 3-joint arm ending in a prismatic slide, and a
+    2-joint head mounted on a massive fixed plate (a movable child of a merged fixed link).
+    Random origins / axes / inertials, shuffled document order; 9 DOF.  floating=True: the
+    torso itself is the root link (no world / base / lift) for RB_MODEL_FLOATING_BASE, 8 DOF
+    + 6 virtual ones (a massless base below a prismatic lift would make H singular).
+    The same seed gives the same torso and branches in both forms."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+
+    def f(x):
+        return " ".join(repr(float(v)) for v in x)
+
+    def inertial(mass):
+        a, b = rng.uniform(0.01, 0.05, 2)
+        c = rng.uniform(abs(a - b) + 0.005, a + b - 0.001)
+        return ("    <inertial>\n"
+                f'      <origin rpy="{f(rng.uniform(-np.pi, np.pi, 3))}" xyz="{f(rng.uniform(-0.1, 0.1, 3))}"/>\n'
+                f'      <mass value="{float(mass)!r}"/>\n'
+                f'      <inertia ixx="{float(a)!r}" ixy="0" ixz="0" iyy="{float(b)!r}" iyz="0" izz="{float(c)!r}"/>\n'
+                "    </inertial>")
+
+    def axis():
+        a = rng.normal(size=3)
+        return a / np.linalg.norm(a)
+
+    links, joints = [], []
+    if not floating:
+        links += ['  <link name="world"/>', '  <link name="base"/>']
+        joints += ['  <joint name="world_joint" type="fixed">\n    <origin rpy="0 0 0" xyz="0 0 0.05"/>\n'
+                   '    <parent link="world"/>\n    <child link="base"/>\n  </joint>']
+
+    def joint(name, kind, parent, child, ax, lim):
+        joints.append(f'  <joint name="{name}" type="{kind}">\n'
+                      f'    <origin rpy="{f(rng.uniform(-np.pi, np.pi, 3))}" xyz="{f(rng.uniform(-0.2, 0.2, 3))}"/>\n'
+                      f'    <parent link="{parent}"/>\n    <child link="{child}"/>\n    <axis xyz="{f(ax)}"/>\n'
+                      f"{lim}\n  </joint>")
+
+    def body(name, mass):
+        links.append(f'  <link name="{name}">\n{inertial(mass)}\n  </link>')
+
+    rev = '    <limit effort="40" lower="-2.5" upper="2.5" velocity="2.0"/>'
+    cont = '    <limit effort="20" velocity="2.0"/>'
+    slide = '    <limit effort="100" lower="-0.2" upper="0.2" velocity="0.5"/>'
+    body("torso", 8.0)
+    if not floating:
+        joint("lift", "prismatic", "base", "torso", (0.0, 0.0, 1.0), slide)
+    else:
+        rng.uniform(-np.pi, np.pi, 3), rng.uniform(-0.2, 0.2, 3)  # keep the random stream aligned
+    body("plate", 1.5)
+    joints.append('  <joint name="plate_mount" type="fixed">\n'
+                  f'    <origin rpy="{f(rng.uniform(-np.pi, np.pi, 3))}" xyz="0 0 0.3"/>\n'
+                  '    <parent link="torso"/>\n    <child link="plate"/>\n  </joint>')
+    parent = "torso"
+    for k, kind in enumerate(("revolute", "revolute", "continuous")):
+        body(f"la{k + 1}", rng.uniform(0.5, 2.0))
+        joint(f"la_j{k + 1}", kind, parent, f"la{k + 1}", axis(), cont if kind == "continuous" else rev)
+        parent = f"la{k + 1}"
+    parent = "torso"
+    for k, kind in enumerate(("revolute", "revolute", "prismatic")):
+        body(f"ra{k + 1}", rng.uniform(0.5, 2.0))
+        joint(f"ra_j{k + 1}", kind, parent, f"ra{k + 1}", axis(), slide if kind == "prismatic" else rev)
+        parent = f"ra{k + 1}"
+    parent = "plate"
+    for k in range(2):
+        body(f"head{k + 1}", rng.uniform(0.3, 1.0))
+        joint(f"head_j{k + 1}", "revolute", parent, f"head{k + 1}", (0.0, 0.0, 1.0) if k == 0 else axis(), rev)
+        parent = f"head{k + 1}"
+    order = rng.permutation(len(joints))
+    return ('<?xml version="1.0"?>\n<robot name="tree9">\n' + "\n".join(links) + "\n"
+            + "\n".join(joints[i] for i in order) + "\n</robot>\n")
+
+
 def input_ranges(limits, kind: str):
     """Per-joint (lo, hi) for kind in {'q','qd','qdd','tau'} from URDF limits (a joint
     without position limits -- continuous -- samples q in [-pi, pi])."""
