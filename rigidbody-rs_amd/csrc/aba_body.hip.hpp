@@ -53,7 +53,7 @@ __device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T
     for (int j = N - 1; j >= 0; --j) {
         const V3<T> ur = v3(IA.A.xz, IA.A.yz, IA.A.zz);
         const V3<T> ul = v3(IA.B.m[6], IA.B.m[7], IA.B.m[8]);
-        const T Dinv = T(1) / IA.A.zz;
+        const T Dinv = recip(IA.A.zz);  // hardware reciprocal (spatial.hip.hpp)
         const T u = tv[j] - pAn.z;
         Drx[j] = ur.x * Dinv; Dry[j] = ur.y * Dinv;
         Dl[j][0] = ul.x * Dinv; Dl[j][1] = ul.y * Dinv; Dl[j][2] = ul.z * Dinv;
