@@ -57,7 +57,8 @@ typedef enum {
 
 /* ---- model construction ------------------------------------------------------- */
 /* Multibody::from_urdf (multibody.rs:65-77) on a file / an in-memory string.  Any
- * number of revolute joints for which a kernel is compiled (multibody_supported_dofs). */
+ * number of revolute joints for which a kernel is compiled (multibody_supported_dofs);
+ * with RB_MODEL_URDF_TREE, trees / prismatic joints of up to 64 DOF (hipRTC kernels). */
 Multibody *multibody_new_from_urdf(const char *path);
 Multibody *multibody_new_from_urdf_string(const char *xml, size_t len);
 
@@ -68,9 +69,18 @@ Multibody *multibody_new_from_urdf_string(const char *xml, size_t len);
  *     results for z-axis chains.  fwd_kin/jac stay in the URDF link frames.
  *   RB_MODEL_URDF_TREE: follow joint parent/child names from the root link; fixed joints
  *     are merged (child inertia into the parent body, origin into the next joint); the
- *     inertial-origin rpy is honoured; revolute/continuous joints only; mimic joints and
- *     branching trees are rejected (RB_ERR_URDF). */
-enum { RB_MODEL_GENERAL_AXES = 1, RB_MODEL_URDF_TREE = 2 };
+ *     inertial-origin rpy is honoured; kinematic trees (links numbered depth-first, parent
+ *     index < child index, multibody_topology) with revolute / continuous / prismatic
+ *     joints; mimic joints are rejected (RB_ERR_URDF).  Trees and prismatic joints run only
+ *     on model-specialised (hipRTC) kernels; fwd_kin / jac then follow the last link's
+ *     ancestor path (other Jacobian columns zero), CRBA keeps the upper-triangle layout
+ *     with exact zeros for unrelated joint pairs.
+ *   RB_MODEL_FLOATING_BASE: a free-floating root body: six massless virtual joints first --
+ *     prismatic along world x, y, z, then revolute about z, y, x (yaw / pitch / roll; the
+ *     root orientation is Rz Ry Rx, singular at pitch = +-pi/2).  Implies the two flags
+ *     above.  Gravity stays the reference's +9.81 base acceleration (multibody.rs:117-120),
+ *     so a free fall reads qdd = (0, 0, -9.81, 0, ...). */
+enum { RB_MODEL_GENERAL_AXES = 1, RB_MODEL_URDF_TREE = 2, RB_MODEL_FLOATING_BASE = 4 };
 Multibody *multibody_new_from_urdf_ex(const char *path, unsigned flags);
 Multibody *multibody_new_from_urdf_string_ex(const char *xml, size_t len, unsigned flags);
 unsigned multibody_flags(const Multibody *mb);
@@ -87,14 +97,18 @@ int multibody_limits(const Multibody *mb, double *lower, double *upper,
                      double *velocity, double *effort);
 /* Writes up to `cap` DOF values the kernels are compiled for; returns their count. */
 int multibody_supported_dofs(int *out, int cap);
+/* Per link: parent link index (-1 = base; the reference's chain has i - 1) and joint type
+ * (0 revolute, 1 prismatic).  Either array may be NULL. */
+int multibody_topology(const Multibody *mb, int *parent, int *joint_type);
 
 /* Uploads the model constants to the current HIP device now (otherwise done lazily on
  * the first batched call); call before capturing batched calls into a hipGraph. */
 int multibody_upload(const Multibody *mb);
 
 /* Which kernel runs for this model on the current device; kind 0 = rnea, 1 = fd,
- * 2 = crba, 3 = rollout.  1 = model-specialised kernel compiled at first use by hipRTC, 0 =
- * precompiled generic kernel (also when hipRTC failed; rb_last_error() holds the log). */
+ * 2 = crba, 3 = rollout, 4 = fwd_kin, 5 = jac.  1 = model-specialised kernel compiled at
+ * first use by hipRTC, 0 = precompiled generic kernel (also when hipRTC failed;
+ * rb_last_error() holds the log -- a tree model's calls then fail with RB_ERR_UNSUPPORTED). */
 int multibody_kernel_path(const Multibody *mb, int kind, int f64);
 int multibody_rnea_kernel_path(const Multibody *mb, int f64);
 /* The generated source of a model-specialised kernel (returns its length; copies at

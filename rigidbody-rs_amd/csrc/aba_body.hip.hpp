@@ -6,7 +6,7 @@
 // (multibody.rs:155-174) -- the reference has no forward-dynamics solve.
 #pragma once
 
-#include "artinertia.hip.hpp"
+#include "tree_body.hip.hpp"
 
 namespace rbamd {
 namespace dev {
@@ -121,7 +121,16 @@ __device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T
     }
 }
 
-template <typename T, int N, bool FAST>
+template <typename T, int N, bool FAST, typename Topo, typename Out>
+__device__ __forceinline__ void aba_any(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
+                                        Out &&out) {
+    if constexpr (Topo::kSerial)
+        aba_eval<T, N, FAST>(mdl, qv, qdv, tv, static_cast<Out &&>(out));
+    else
+        aba_eval_tree<T, N, FAST, Topo>(mdl, qv, qdv, tv, static_cast<Out &&>(out));
+}
+
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
                                          const T *__restrict__ tau, T *__restrict__ qdd, uint32_t b,
                                          int64_t ld) {
@@ -143,7 +152,7 @@ __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, 
         tv[j] = ld_row(tau, j * ld, off);
         __builtin_amdgcn_sched_barrier(0);
     }
-    aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
+    aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
 }
 
 // Resident grid-stride form (A/B, model-specialised kernels): each lane walks the batch
@@ -152,7 +161,7 @@ __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, 
 // latency hidden behind pass 1.  Block k of pass i covers configurations
 // (k + i * gridDim.x) * 256 + [0, 256); the tiled / SoA block base is o(b0) =
 // (b0 / 256) * bs + b0 % 256 as in the lane kernels.
-template <typename T, int N, bool FAST>
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void aba_stream(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
                                            const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
                                            int64_t ld, int64_t bs) {
@@ -184,7 +193,7 @@ __device__ __forceinline__ void aba_stream(const T *mdl, const T *__restrict__ q
 #pragma unroll
             for (int j = 0; j < N; ++j) tv[j] = ld_row(tau + base(blk), j * ld, off);
             T *out = qdd + base(blk);
-            aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(out, j * ld, off, v); });
+            aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(out, j * ld, off, v); });
         }
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -217,7 +226,7 @@ struct RolloutShared {
     T x[rollout_lds_state<T, N>() ? 2 * N * kRolloutBlock : 1];
 };
 
-template <typename T, int N, bool FAST>
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T *__restrict__ qd,
                                              const T *__restrict__ tau_seq, T dt, int K, T *__restrict__ traj,
                                              uint32_t b, int64_t ld, RolloutShared<T, N> &sh) {
@@ -238,7 +247,7 @@ __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T 
                 tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
             }
             // aba_eval fences memory before its last pass, so these re-read LDS.
-            aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T a) {
+            aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T a) {
                 const T qdn = fmadd(dt, a, sx[(N + j) * kRolloutBlock]);
                 const T qn = fmadd(dt, qdn, sx[j * kRolloutBlock]);
                 sx[(N + j) * kRolloutBlock] = qdn;
@@ -262,7 +271,7 @@ __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T 
             T tv[N], a[N];
 #pragma unroll
             for (int j = 0; j < N; ++j) tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
-            aba_eval<T, N, FAST>(mdl, qv, qdv, tv, [&](int j, T v) { a[j] = v; });
+            aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T v) { a[j] = v; });
 #pragma unroll
             for (int j = 0; j < N; ++j) {
                 qdv[j] = fmadd(dt, a[j], qdv[j]);

@@ -26,11 +26,15 @@
 
 #include "fr3_embedded.inc"  // kFr3Urdf: compact FR3 description (tools/gen_fixtures.py)
 
-#define RB_VERSION "rigidbody-rs_amd 0.1.0 (gfx950)"
+#define RB_VERSION "rigidbody-rs_amd 0.2.0 (gfx950)"
+
+static const char *const kKindMsg = "kind must be 0 rnea, 1 fd, 2 crba, 3 rollout, 4 fwd_kin or 5 jac";
 
 namespace {
 
 thread_local std::string g_last_error;
+// Why a launcher refused (a tree model without its hipRTC kernel); hip_err reports it.
+thread_local std::string t_launch_note;
 
 int set_err(int code, const std::string &msg) {
     g_last_error = msg;
@@ -38,8 +42,13 @@ int set_err(int code, const std::string &msg) {
 }
 
 int hip_err(hipError_t e, const char *where) {
-    return set_err(RB_ERR_HIP, std::string(where) + ": " + hipGetErrorName(e) + " (" +
-                                   hipGetErrorString(e) + ")");
+    std::string msg = std::string(where) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+    if (!t_launch_note.empty()) {
+        msg += ": " + t_launch_note;
+        t_launch_note.clear();
+        return set_err(RB_ERR_UNSUPPORTED, msg);
+    }
+    return set_err(RB_ERR_HIP, msg);
 }
 
 bool env_flag(const char *name, bool dflt) {
@@ -74,6 +83,8 @@ struct Multibody {
 
 namespace {
 
+constexpr int kMaxTreeDof = 64;
+
 Multibody *make(rbamd::Model &&m) {
     if (!m.axes_supported()) {
         set_err(RB_ERR_UNSUPPORTED,
@@ -81,8 +92,12 @@ Multibody *make(rbamd::Model &&m) {
                 "(multibody.rs:130-138,144); pass RB_MODEL_GENERAL_AXES for general axes");
         return nullptr;
     }
-    if (!rbamd::dof_supported(m.n)) {
-        set_err(RB_ERR_DOF, "no kernel compiled for " + std::to_string(m.n) + " DOF");
+    // The reference's serial revolute chains run on the precompiled kernels (dofs.hpp) or
+    // their model-specialised versions; trees and prismatic joints only on the latter, which
+    // exist for any DOF count.
+    if (m.serial_revolute() ? !rbamd::dof_supported(m.n) : m.n > kMaxTreeDof) {
+        set_err(RB_ERR_DOF, m.serial_revolute() ? "no kernel compiled for " + std::to_string(m.n) + " DOF"
+                                                : "tree models support at most 64 DOF, got " + std::to_string(m.n));
         return nullptr;
     }
     Multibody *mb = new Multibody();
@@ -157,6 +172,21 @@ const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast) {
     return jit_get(mb, rbamd::JitKind::Rnea, f64, fast);
 }
 
+// A tree / prismatic model has no precompiled kernel: without its hipRTC kernel the launch
+// is refused (hipErrorNotSupported, reported as RB_ERR_UNSUPPORTED with the reason).
+hipError_t no_generic(const Multibody *mb) {
+    std::string why = "kinematic-tree / prismatic models run only on model-specialised (hipRTC) kernels";
+    if (!rbamd::jit_enabled()) {
+        why += ", which are disabled (RB_JIT=0 / rb_set_tuning(\"jit\", 0))";
+    } else {
+        std::lock_guard<std::mutex> lk(mb->mu);
+        for (auto &kv : mb->jit)
+            if (!kv.second.error.empty()) why += "; hipRTC: " + kv.second.error.substr(0, 400);
+    }
+    t_launch_note = why;
+    return hipErrorNotSupported;
+}
+
 hipError_t jit_launch(const rbamd::JitKernel *jk, hipFunction_t fn, uint32_t B, void **args, hipStream_t s) {
     const unsigned full = (B + 255u) / 256u;
     unsigned g = full;
@@ -185,6 +215,7 @@ hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const 
             fn = jk->tile_function;
         return jit_launch(jk, fn, B, args, s);
     }
+    if (!mb->model.serial_revolute()) return no_generic(mb);
     return rbamd::launch_rnea<T>(mb->model.n, mdl, q, qd, qdd, tau, B, ld, s, fast_trig(), tiled);
 }
 
@@ -197,6 +228,7 @@ hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T 
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau, (void *)&qdd, (void *)&B, (void *)&lda, (void *)&bs};
         return jit_launch(jk, jk->function, B, args, s);
     }
+    if (!mb->model.serial_revolute()) return no_generic(mb);
     return rbamd::launch_aba<T>(mb->model.n, mdl, q, qd, tau, qdd, B, ld, s, fast_trig(), tiled);
 }
 
@@ -209,6 +241,7 @@ hipError_t launch_rollout_any(const Multibody *mb, const T *mdl, T *q, T *qd, co
                         (void *)&B, (void *)&ld};
         return jit_launch(jk, jk->function, B, args, s);
     }
+    if (!mb->model.serial_revolute()) return no_generic(mb);
     return rbamd::launch_rollout<T>(mb->model.n, mdl, q, qd, tau_seq, dt, K, traj, B, ld, s, fast_trig());
 }
 
@@ -220,7 +253,22 @@ hipError_t launch_crba_any(const Multibody *mb, const T *mdl, const T *q, T *H, 
         void *args[] = {(void *)&q, (void *)&H, (void *)&B, (void *)&ld};
         return jit_launch(jk, jk->function, B, args, s);
     }
+    if (!mb->model.serial_revolute()) return no_generic(mb);
     return rbamd::launch_crba<T>(mb->model.n, mdl, q, H, B, ld, s);
+}
+
+// fwd_kin / jac (fp64): the precompiled kernels for serial revolute chains, hipRTC kernels
+// (tree_body.hip.hpp) for trees and prismatic joints.
+hipError_t launch_kin_any(const Multibody *mb, bool jac, const double *mdl, const double *q, double *out, uint32_t B,
+                          int64_t ld, hipStream_t s) {
+    if (B == 0) return hipSuccess;
+    if (mb->model.serial_revolute())
+        return jac ? rbamd::launch_jac<double>(mb->model.n, mdl, q, out, B, ld, s)
+                   : rbamd::launch_fwd_kin<double>(mb->model.n, mdl, q, out, B, ld, s);
+    const rbamd::JitKernel *jk = jit_get(mb, jac ? rbamd::JitKind::Jac : rbamd::JitKind::FwdKin, true, false);
+    if (!jk) return no_generic(mb);
+    void *args[] = {(void *)&q, (void *)&out, (void *)&B, (void *)&ld};
+    return jit_launch(jk, jk->function, B, args, s);
 }
 
 constexpr int64_t kChunk = int64_t(1) << 28;  // per-launch batch cap: b * sizeof(T) < 2^32
@@ -509,7 +557,7 @@ double *multibody_fwd_kin(const Multibody *mb, const double *q) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
         if (rc) return rc;
-        hipError_t e = rbamd::launch_fwd_kin<double>((int)n, mdl, din, dout, 1, 1, s);
+        hipError_t e = launch_kin_any(mb, false, mdl, din, dout, 1, 1, s);
         return e == hipSuccess ? RB_OK : hip_err(e, "fwd_kin launch");
     });
 }
@@ -521,7 +569,7 @@ double *multibody_jac(const Multibody *mb, const double *q) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
         if (rc) return rc;
-        hipError_t e = rbamd::launch_jac<double>((int)n, mdl, din, dout, 1, 1, s);
+        hipError_t e = launch_kin_any(mb, true, mdl, din, dout, 1, 1, s);
         return e == hipSuccess ? RB_OK : hip_err(e, "jac launch");
     });
 }
@@ -595,11 +643,21 @@ int multibody_limits(const Multibody *mb, double *lower, double *upper, double *
 
 int multibody_supported_dofs(int *out, int cap) { return rbamd::supported_dofs(out, cap); }
 
+int multibody_topology(const Multibody *mb, int *parent, int *joint_type) {
+    if (!mb) return set_err(RB_ERR_NULL, "NULL Multibody handle");
+    for (int i = 0; i < mb->model.n; ++i) {
+        if (parent) parent[i] = mb->model.links[i].parent;
+        if (joint_type) joint_type[i] = mb->model.links[i].type;
+    }
+    return RB_OK;
+}
+
 int multibody_kernel_path(const Multibody *mb, int kind, int f64) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 3) return -set_err(RB_ERR_ARG, "kind must be 0 rnea, 1 fd, 2 crba or 3 rollout");
+    if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
+    if (kind >= 4 && (!f64 || mb->model.serial_revolute())) return 0;  // precompiled fp64 kinematics
     if (!rbamd::jit_enabled()) return 0;
-    if (jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 ? false : fast_trig())) return 1;
+    if (jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 || kind >= 4 ? false : fast_trig())) return 1;
     int d = 0;
     (void)hipGetDevice(&d);
     std::lock_guard<std::mutex> lk(mb->mu);
@@ -612,9 +670,9 @@ int multibody_rnea_kernel_path(const Multibody *mb, int f64) { return multibody_
 
 int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 3) return -set_err(RB_ERR_ARG, "kind must be 0 rnea, 1 fd, 2 crba or 3 rollout");
+    if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
     const std::string src = rbamd::jit_source(mb->model, (rbamd::JitKind)kind, f64 != 0,
-                                              kind != 2 && fast_trig() && !f64,
+                                              kind != 2 && kind < 4 && fast_trig() && !f64,
                                               jit_stream((rbamd::JitKind)kind, f64 != 0, mb->model.n));
     if (buf && cap > 0) {
         const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
@@ -626,10 +684,10 @@ int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int6
 
 int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char *arch) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 3) return -set_err(RB_ERR_ARG, "kind must be 0 rnea, 1 fd, 2 crba or 3 rollout");
+    if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
     std::vector<char> code;
     std::string err;
-    if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && fast_trig() && !f64,
+    if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && kind < 4 && fast_trig() && !f64,
                             jit_stream((rbamd::JitKind)kind, f64 != 0, mb->model.n),
                             arch ? arch : "gfx950", &code, &err))
         return -set_err(RB_ERR_HIP, err);
@@ -767,7 +825,7 @@ int multibody_fwd_kin_batch_f64(const Multibody *mb, const double *q, double *po
     const double *mdl = nullptr;
     if ((rc = device_consts<double>(mb, &mdl))) return rc;
     return chunked<double>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = rbamd::launch_fwd_kin<double>(mb->model.n, mdl, q + b0, pos + b0, nb, ld, (hipStream_t)stream);
+        hipError_t e = launch_kin_any(mb, false, mdl, q + b0, pos + b0, nb, ld, (hipStream_t)stream);
         return e == hipSuccess ? RB_OK : hip_err(e, "fwd_kin launch");
     });
 }
@@ -781,7 +839,7 @@ int multibody_jac_batch_f64(const Multibody *mb, const double *q, double *J, int
     const double *mdl = nullptr;
     if ((rc = device_consts<double>(mb, &mdl))) return rc;
     return chunked<double>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = rbamd::launch_jac<double>(mb->model.n, mdl, q + b0, J + b0, nb, ld, (hipStream_t)stream);
+        hipError_t e = launch_kin_any(mb, true, mdl, q + b0, J + b0, nb, ld, (hipStream_t)stream);
         return e == hipSuccess ? RB_OK : hip_err(e, "jac launch");
     });
 }

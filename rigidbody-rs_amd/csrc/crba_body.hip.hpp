@@ -4,7 +4,7 @@
 // column-major matrix, H[j + n*i] for j <= i, strictly-lower entries exact zeros.
 #pragma once
 
-#include "artinertia.hip.hpp"
+#include "tree_body.hip.hpp"
 
 namespace rbamd {
 namespace dev {
@@ -42,14 +42,17 @@ __device__ __forceinline__ void crba_eval(const T *mdl, const T (&qv)[N], Out &&
     }
 }
 
-template <typename T, int N, bool FAST>
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void crba_lane(const T *mdl, const T *__restrict__ q, T *__restrict__ H, uint32_t b,
                                           int64_t ld) {
     const uint32_t off = b * (uint32_t)sizeof(T);
     T qv[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) qv[j] = ld_row(q, j * ld, off);
-    crba_eval<T, N, FAST>(mdl, qv, [&](int e, T v) { st_row(H, e * ld, off, v); });
+    if constexpr (Topo::kSerial)
+        crba_eval<T, N, FAST>(mdl, qv, [&](int e, T v) { st_row(H, e * ld, off, v); });
+    else
+        crba_eval_tree<T, N, FAST, Topo>(mdl, qv, [&](int e, T v) { st_row(H, e * ld, off, v); });
 }
 
 }  // namespace dev

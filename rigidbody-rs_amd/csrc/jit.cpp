@@ -80,9 +80,28 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
     o << (kind == JitKind::Rnea                               ? "#include \"rnea_body.hip.hpp\"\n"
           : (kind == JitKind::Fd || kind == JitKind::Rollout) ? "#include \"aba_body.hip.hpp\"\n"
-                                                              : "#include \"crba_body.hip.hpp\"\n");
+          : kind == JitKind::Crba                             ? "#include \"crba_body.hip.hpp\"\n"
+                                                              : "#include \"tree_body.hip.hpp\"\n");
     o << "using T = " << (f64 ? "double" : "float") << ";\n";
     o << "constexpr int N = " << m.n << ";\n";
+    // Topology policy (tree_body.hip.hpp): the tuned serial code for the reference's chain,
+    // else the tree forms with every parent index / joint type a compile-time constant.
+    if (m.serial_revolute()) {
+        o << "using Topo = rbamd::dev::SerialTopo;\n";
+    } else {
+        o << "struct Topo {\n  static constexpr bool kSerial = false;\n  static constexpr int kPar[N] = {";
+        for (int i = 0; i < m.n; ++i) o << (i ? ", " : "") << m.links[i].parent;
+        o << "};\n  static constexpr int kPri[N] = {";
+        for (int i = 0; i < m.n; ++i) o << (i ? ", " : "") << (m.links[i].type == kJointPrismatic ? 1 : 0);
+        o << "};\n"
+             "  static constexpr int parent(int j) { return kPar[j]; }\n"
+             "  static constexpr bool prismatic(int j) { return kPri[j] != 0; }\n"
+             "  static constexpr int last_child(int j) { int c = -1; for (int k = j + 1; k < N; ++k) if (kPar[k] == j) c = k; return c; }\n"
+             "  static constexpr bool is_ancestor(int a, int i) { for (int k = kPar[i]; k >= 0; k = kPar[k]) if (k == a) return true; return false; }\n"
+             "  static constexpr int child_toward(int a, int i) { int c = i; for (int k = kPar[i]; k >= 0; c = k, k = kPar[k]) if (k == a) return c; return -1; }\n"
+             "  static constexpr bool on_path(int j) { return j == N - 1 || is_ancestor(j, N - 1); }\n"
+             "};\n";
+    }
     o << "static __device__ constexpr T kModel[" << pk.size() << "] = {\n";
     for (size_t k = 0; k < pk.size(); ++k) o << "  " << literal(pk[k], f64) << ",\n";
     o << "};\n";
@@ -102,10 +121,10 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
             o << "  T qv[N], qdv[N], qddv[N];\n";
             o << "  rbamd::dev::load_cfg<T, N>(q, qd, qdd, ld, b * (uint32_t)sizeof(T), qv, qdv, qddv);\n";
             o << "  rbamd::dev::rnea_stream_lane<T, N, " << F
-              << ">(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
+              << ", Topo>(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
         } else {
             o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
-            o << "  rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
+            o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
         }
         o << "}\n";
         if (jit_tile_ok(m.n, f64)) {  // SoA only
@@ -114,22 +133,22 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
             o << "  __shared__ T tile[3 * N * 256];\n";
             o << "  const uint32_t b0 = blockIdx.x * 256u;\n";
             o << "  if (b0 + 256u <= B) {\n";
-            o << "    rbamd::dev::rnea_tile<T, N, " << F << ">(kModel, q, qd, qdd, tau, b0, ld, tile);\n";
+            o << "    rbamd::dev::rnea_tile<T, N, " << F << ", Topo>(kModel, q, qd, qdd, tau, b0, ld, tile);\n";
             o << "  } else {\n";
             o << "    const uint32_t b = b0 + threadIdx.x;\n";
-            o << "    if (b < B) rbamd::dev::rnea_lane<T, N, " << F << ">(kModel, q, qd, qdd, tau, b, ld);\n";
+            o << "    if (b < B) rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q, qd, qdd, tau, b, ld);\n";
             o << "  }\n}\n";
         }
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
         if (stream) {
-            o << "  rbamd::dev::aba_stream<T, N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
+            o << "  rbamd::dev::aba_stream<T, N, " << F << ", Topo>(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
         } else {
             o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
             o << "  if (b >= B) return;\n";
             o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
-            o << "  rbamd::dev::aba_lane<T, N, " << F << ">(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
+            o << "  rbamd::dev::aba_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
         }
     } else if (kind == JitKind::Rollout) {
         o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
@@ -137,12 +156,18 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         o << "  __shared__ rbamd::dev::RolloutShared<T, N> sh;\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
-        o << "  rbamd::dev::rollout_lane<T, N, " << F << ">(kModel, q, qd, tau_seq, dt, K, traj, b, ld, sh);\n}\n";
+        o << "  rbamd::dev::rollout_lane<T, N, " << F << ", Topo>(kModel, q, qd, tau_seq, dt, K, traj, b, ld, sh);\n}\n";
+    } else if (kind == JitKind::FwdKin || kind == JitKind::Jac) {
+        o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ out, uint32_t B, int64_t ld) {\n";
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        o << "  rbamd::dev::" << (kind == JitKind::FwdKin ? "fwd_kin" : "jac") << "_lane_tree<T, N, " << F
+          << ", Topo>(kModel, q, out, b, ld);\n}\n";
     } else {
         o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ H, uint32_t B, int64_t ld) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
-        o << "  rbamd::dev::crba_lane<T, N, " << F << ">(kModel, q, H, b, ld);\n}\n";
+        o << "  rbamd::dev::crba_lane<T, N, " << F << ", Topo>(kModel, q, H, b, ld);\n}\n";
     }
     return o.str();
 }

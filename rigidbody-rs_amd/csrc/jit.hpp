@@ -23,7 +23,9 @@
 
 namespace rbamd {
 
-enum class JitKind : int { Rnea = 0, Fd = 1, Crba = 2, Rollout = 3 };
+// FwdKin / Jac: built only for models the precompiled kinematics kernels cannot express
+// (kinematic trees, prismatic joints -- Model::serial_revolute() false).
+enum class JitKind : int { Rnea = 0, Fd = 1, Crba = 2, Rollout = 3, FwdKin = 4, Jac = 5 };
 
 struct JitKernel {
     hipModule_t module = nullptr;

@@ -12,7 +12,8 @@ enum : int {
     kM = 12,    // mass
     kH = 13,    // first mass moment h = m * com (3)
     kIo = 16,   // inertia about the link origin, symmetric: xx xy xz yy yz zz (6)
-    kPad = 22,  // 2 unused
+    kParent = 22,  // parent link index (-1: base) -- informational, kernels take topology
+    kType = 23,    // joint type (0 revolute, 1 prismatic)  at compile time (jit.cpp)
 };
 
 // After the n link blocks: kTailOut scalars, the rotation R0 (row-major) that starts the

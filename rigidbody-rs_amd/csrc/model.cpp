@@ -228,93 +228,140 @@ struct Body {
     }
 };
 
-bool movable(const std::string &type) { return type == "revolute" || type == "continuous"; }
+bool movable(const std::string &type) {
+    return type == "revolute" || type == "continuous" || type == "prismatic";
+}
 
-// kModelUrdfTree reading (see model.hpp).
-Model chain_from_tree(const UrdfRobot &robot) {
-    std::vector<int> as_child(robot.links.size(), 0);
-    auto link_index = [&](const std::string &name) {
-        for (size_t k = 0; k < robot.links.size(); ++k)
-            if (robot.links[k].name == name) return (int)k;
-        throw std::runtime_error("joint refers to unknown link '" + name + "'");
-    };
-    for (const UrdfJoint &j : robot.joints) {
-        link_index(j.parent);
-        as_child[link_index(j.child)]++;
-    }
-    int root = -1;
-    for (size_t k = 0; k < robot.links.size(); ++k) {
-        if (as_child[k] > 1) throw std::runtime_error("link '" + robot.links[k].name + "' has several parents");
-        if (as_child[k] == 0) {
-            if (root >= 0) throw std::runtime_error("URDF has several root links");
-            root = (int)k;
+// kModelUrdfTree reading (see model.hpp).  Links are numbered depth-first (preorder): a
+// body's movable child joints in the order a stack walk of its fixed subtree meets them
+// (each link's joints in document order), so parent indices are always smaller.  The same
+// numbering as oracle/urdf_model.py model_frames_from_urdf_tree.
+class TreeReader {
+  public:
+    explicit TreeReader(const UrdfRobot &robot) : robot_(robot) {}
+
+    Model read(bool floating) {
+        std::vector<int> as_child(robot_.links.size(), 0);
+        for (const UrdfJoint &j : robot_.joints) {
+            link_index(j.parent);
+            as_child[link_index(j.child)]++;
         }
+        int root = -1;
+        for (size_t k = 0; k < robot_.links.size(); ++k) {
+            if (as_child[k] > 1) throw std::runtime_error("link '" + robot_.links[k].name + "' has several parents");
+            if (as_child[k] == 0) {
+                if (root >= 0) throw std::runtime_error("URDF has several root links");
+                root = (int)k;
+            }
+        }
+        if (root < 0) throw std::runtime_error("URDF has no root link");
+        Body root_body;
+        std::vector<Child> kids = body(root, &root_body);
+        int base = -1;
+        if (floating) {
+            // virtual joints: prismatic x, y, z (world axes), revolute z, y, x (yaw, pitch,
+            // roll); the root body rides on the last one.  Limits shape test inputs only.
+            static const double ax[6][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 1}, {0, 1, 0}, {1, 0, 0}};
+            static const double lim[6][3] = {{-1, 1, 1}, {-1, 1, 1}, {-1, 1, 1},
+                                             {-M_PI, M_PI, 2}, {-1.2, 1.2, 2}, {-M_PI, M_PI, 2}};
+            for (int k = 0; k < 6; ++k) {
+                LinkModel L{};
+                std::memcpy(L.axis, ax[k], sizeof L.axis);
+                L.pq[3] = 1.0;
+                L.lower = lim[k][0];
+                L.upper = lim[k][1];
+                L.velocity = lim[k][2];
+                L.effort = 1000.0;
+                L.parent = k - 1;
+                L.type = k < 3 ? kJointPrismatic : kJointRevolute;
+                m_.links.push_back(L);
+            }
+            root_body.to_link(m_.links[5]);
+            base = 5;
+        }
+        for (const Child &c : kids) visit(c, base);
+        return std::move(m_);
     }
-    if (root < 0) throw std::runtime_error("URDF has no root link");
-    Model m;
-    int cur = root;
-    bool base = true;
-    LinkModel pending{};
-    for (;;) {
-        // the current body = link `cur` + its fixed-joint subtree; find its one movable child
-        Body body;
-        const UrdfJoint *next = nullptr;
-        Frame next_frame;
-        std::vector<std::pair<int, Frame>> stack{{cur, Frame{}}};
+
+  private:
+    struct Child {
+        const UrdfJoint *joint;
+        Frame frame;  // joint origin in the parent body's frame
+    };
+
+    int link_index(const std::string &name) const {
+        for (size_t k = 0; k < robot_.links.size(); ++k)
+            if (robot_.links[k].name == name) return (int)k;
+        throw std::runtime_error("joint refers to unknown link '" + name + "'");
+    }
+
+    // Link `root` plus its fixed-joint subtree, accumulated into *out; returns its movable
+    // child joints.
+    std::vector<Child> body(int root, Body *out) const {
+        std::vector<Child> kids;
+        std::vector<std::pair<int, Frame>> stack{{root, Frame{}}};
         while (!stack.empty()) {
             const auto [ln, T] = stack.back();
             stack.pop_back();
-            body.add(robot.links[ln], T);
-            for (const UrdfJoint &j : robot.joints) {
-                if (j.parent != robot.links[ln].name) continue;
+            out->add(robot_.links[ln], T);
+            for (const UrdfJoint &j : robot_.joints) {
+                if (j.parent != robot_.links[ln].name) continue;
                 if (j.mimic) throw std::runtime_error("mimic joint '" + j.name + "' is not supported");
                 const Frame Tj = compose(T, joint_origin(j));
                 if (j.type == "fixed") {
                     stack.push_back({link_index(j.child), Tj});
                 } else if (movable(j.type)) {
-                    if (next)
-                        throw std::runtime_error("branching tree at '" + robot.links[ln].name +
-                                                 "': only serial chains are supported");
-                    next = &j;
-                    next_frame = Tj;
+                    kids.push_back({&j, Tj});
                 } else {
                     throw std::runtime_error("joint '" + j.name + "' of type '" + j.type + "' is not supported");
                 }
             }
         }
-        if (!base) {
-            body.to_link(pending);
-            m.links.push_back(pending);
-        }
-        if (!next) break;
-        pending = LinkModel{};
-        const double *a = next->axis;
-        const double an = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
-        if (!(an > 0.0)) throw std::runtime_error("joint '" + next->name + "' has a zero axis");
-        for (int k = 0; k < 3; ++k) pending.axis[k] = a[k] / an;
-        quat_from_matrix(next_frame.R, pending.pq);
-        std::memcpy(pending.pt, next_frame.t, sizeof pending.pt);
-        pending.lower = next->lower;
-        pending.upper = next->upper;
-        pending.velocity = next->velocity;
-        pending.effort = next->effort;
-        cur = link_index(next->child);
-        base = false;
+        return kids;
     }
-    return m;
-}
+
+    void visit(const Child &c, int parent) {
+        const UrdfJoint &j = *c.joint;
+        LinkModel L{};
+        const double *a = j.axis;
+        const double an = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        if (!(an > 0.0)) throw std::runtime_error("joint '" + j.name + "' has a zero axis");
+        for (int k = 0; k < 3; ++k) L.axis[k] = a[k] / an;
+        quat_from_matrix(c.frame.R, L.pq);
+        std::memcpy(L.pt, c.frame.t, sizeof L.pt);
+        L.lower = j.lower;
+        L.upper = j.upper;
+        L.velocity = j.velocity;
+        L.effort = j.effort;
+        L.parent = parent;
+        L.type = j.type == "prismatic" ? kJointPrismatic : kJointRevolute;
+        const int idx = (int)m_.links.size();
+        m_.links.push_back(L);
+        Body b;
+        const std::vector<Child> kids = body(link_index(j.child), &b);
+        b.to_link(m_.links[idx]);
+        for (const Child &k : kids) visit(k, idx);
+    }
+
+    const UrdfRobot &robot_;
+    Model m_;
+};
 
 }  // namespace
 
 Model Model::from_urdf_text(const std::string &xml, unsigned flags) {
     if (flags & ~kModelFlagsAll) throw std::runtime_error("unknown model flags");
+    if (flags & kModelFloatingBase) flags |= kModelUrdfTree | kModelGeneralAxes;
     UrdfRobot robot = parse_urdf(xml);
     Model m;
     if (flags & kModelUrdfTree) {
-        m = chain_from_tree(robot);
+        m = TreeReader(robot).read((flags & kModelFloatingBase) != 0);
     } else {
         std::vector<RawJoint> chain = select_chain(robot, &m.pairing_matches_child);
-        for (const RawJoint &rj : chain) m.links.push_back(link_from_urdf(rj));
+        for (const RawJoint &rj : chain) {
+            m.links.push_back(link_from_urdf(rj));
+            m.links.back().parent = (int)m.links.size() - 2;  // multibody.rs: a serial chain
+        }
     }
     if (m.links.empty()) throw std::runtime_error("URDF has no non-fixed joint");
     m.n = (int)m.links.size();
@@ -325,7 +372,7 @@ Model Model::from_urdf_text(const std::string &xml, unsigned flags) {
 std::vector<double> Model::blob() const {
     std::vector<double> b(kBlobHeader + (size_t)n * kBlobPerLink, 0.0);
     b[0] = kBlobMagic;
-    b[1] = 2.0;
+    b[1] = 3.0;
     b[2] = (double)n;
     b[3] = pairing_matches_child ? 1.0 : 0.0;
     b[4] = (double)flags;
@@ -343,13 +390,15 @@ std::vector<double> Model::blob() const {
         p[33] = L.upper;
         p[34] = L.velocity;
         p[35] = L.effort;
+        p[36] = (double)L.parent;
+        p[37] = (double)L.type;
     }
     return b;
 }
 
 Model Model::from_blob(const double *b, int64_t len) {
-    if (!b || len < kBlobHeader || b[0] != kBlobMagic || b[1] != 2.0)
-        throw std::runtime_error("not a rigidbody model blob");
+    if (!b || len < kBlobHeader || b[0] != kBlobMagic || b[1] != 3.0)
+        throw std::runtime_error("not a rigidbody model blob (version 3)");
     const int n = (int)b[2];
     if (n < 1 || len != kBlobHeader + (int64_t)n * kBlobPerLink)
         throw std::runtime_error("model blob has the wrong length");
@@ -374,6 +423,10 @@ Model Model::from_blob(const double *b, int64_t len) {
         L.upper = p[33];
         L.velocity = p[34];
         L.effort = p[35];
+        L.parent = (int)p[36];
+        L.type = (int)p[37];
+        if (p[36] != (double)L.parent || L.parent < -1 || L.parent >= i || (L.type != kJointRevolute && L.type != kJointPrismatic))
+            throw std::runtime_error("model blob has a bad topology");
     }
     return m;
 }
@@ -382,6 +435,12 @@ bool Model::all_axes_z() const {
     for (const LinkModel &L : links)
         if (std::fabs(L.axis[0]) > 1e-12 || std::fabs(L.axis[1]) > 1e-12 || L.axis[2] <= 0.0)
             return false;
+    return true;
+}
+
+bool Model::serial_revolute() const {
+    for (int i = 0; i < n; ++i)
+        if (links[i].parent != i - 1 || links[i].type != kJointRevolute) return false;
     return true;
 }
 
@@ -397,13 +456,17 @@ namespace {
 template <typename T>
 std::vector<T> pack(const Model &m) {
     std::vector<T> out((size_t)m.n * kLinkStride + kTailOut, T(0));
+    std::vector<double> Ras((size_t)m.n * 9);
     double Rprev[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // base frame: no axis change
     for (int i = 0; i < m.n; ++i) {
         const LinkModel &L = m.links[i];
         T *p = &out[(size_t)i * kLinkStride];
         double R[9], Ra[9], pt[3], com[3], io[9];
+        static const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        std::memcpy(Rprev, L.parent >= 0 ? &Ras[(size_t)L.parent * 9] : I3, sizeof Rprev);
         quat_to_matrix(L.pq, R);
         axis_frame(L.axis, Ra);
+        std::memcpy(&Ras[(size_t)i * 9], Ra, sizeof Ra);
         std::memcpy(pt, L.pt, sizeof pt);
         std::memcpy(com, L.com, sizeof com);
         std::memcpy(io, L.io, sizeof io);
@@ -418,7 +481,6 @@ std::vector<T> pack(const Model &m) {
             mat_mul(At, L.io, tmp);
             mat_mul(tmp, Ra, io);
         }
-        std::memcpy(Rprev, Ra, sizeof Ra);
         for (int k = 0; k < 9; ++k) p[kE0 + k] = (T)R[k];
         for (int k = 0; k < 3; ++k) p[kP + k] = (T)pt[k];
         p[kM] = (T)L.mass;
@@ -429,7 +491,10 @@ std::vector<T> pack(const Model &m) {
         p[kIo + 3] = (T)io[4];
         p[kIo + 4] = (T)io[5];
         p[kIo + 5] = (T)io[8];
+        p[kParent] = (T)L.parent;
+        p[kType] = (T)L.type;
     }
+    std::memcpy(Rprev, &Ras[(size_t)(m.n - 1) * 9], sizeof Rprev);  // the last link's axis frame
     // Jacobian start rotation: R_a of the last link, transposed (kinematics.hip jac_kernel)
     T *tail = &out[(size_t)m.n * kLinkStride];
     for (int r = 0; r < 3; ++r)

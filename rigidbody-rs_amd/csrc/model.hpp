@@ -18,7 +18,7 @@
 namespace rbamd {
 
 constexpr int kBlobHeader = 5;    // magic, version, n, index-pairing flag, model flags
-constexpr int kBlobPerLink = 36;  // see Model::blob
+constexpr int kBlobPerLink = 38;  // see Model::blob
 constexpr double kBlobMagic = 20250224.0;
 
 struct LinkModel {
@@ -30,7 +30,13 @@ struct LinkModel {
     double icom[9];  // about COM, row-major
     double io[9];    // about link origin, row-major
     double lower, upper, velocity, effort;
+    // Kinematic tree (beyond the reference's serial chain): parent link
+    // index (-1 = the fixed base; always < this link's index) and joint type.
+    int parent = -1;
+    int type = 0;  // kJointRevolute / kJointPrismatic
 };
+
+enum : int { kJointRevolute = 0, kJointPrismatic = 1 };
 
 // Model-reading flags (rigidbody_batch.h RB_MODEL_*).
 enum : unsigned {
@@ -41,10 +47,13 @@ enum : unsigned {
     // Physical URDF tree instead of the reference's index pairing (multibody.rs:70):
     // follow joint parent/child names from the root link, merge fixed joints (their
     // child bodies join the parent body, their origins compose into the next joint),
-    // honour the inertial-origin rpy, accept revolute/continuous joints only, reject
-    // mimic joints and branching (>1 movable subtree per body).
+    // honour the inertial-origin rpy.  Kinematic trees (links numbered depth-first, parents
+    // first) and revolute / continuous / prismatic joints; mimic joints are rejected.
     kModelUrdfTree = 2u,
-    kModelFlagsAll = 3u,
+    // Free-floating root: six massless virtual joints (prismatic x, y, z; revolute z, y, x)
+    // between the world and the root body.  Implies kModelUrdfTree | kModelGeneralAxes.
+    kModelFloatingBase = 4u,
+    kModelFlagsAll = 7u,
 };
 
 struct Model {
@@ -59,13 +68,18 @@ struct Model {
     std::vector<double> blob() const;
 
     bool all_axes_z() const;
+    // The reference's topology: parent(i) = i - 1 and every joint revolute.  Only such
+    // models run on the precompiled generic kernels; trees and prismatic joints need the
+    // model-specialised (hipRTC) ones.
+    bool serial_revolute() const;
     // Every axis usable under `flags`: +z always, any direction with kModelGeneralAxes.
     bool axes_supported() const;
     double total_mass() const;
 
     // Device constants: n * kLinkStride scalars laid out per link as layout.hpp says, then
     // kTailOut.  A link whose axis is not +z is re-expressed in a frame whose z is its
-    // axis (R_a e_z = axis): R_p' = R_a,parent^T R_p R_a, p' = R_a,parent^T p,
+    // axis (R_a e_z = axis): R_p' = R_a,parent^T R_p R_a, p' = R_a,parent^T p (parent = the
+    // link's tree parent, identity for the base),
     // c' = R_a^T c, I' = R_a^T I R_a -- so the kernels' z-joint code is exact for any axis.
     std::vector<float> pack_f32() const;
     std::vector<double> pack_f64() const;

@@ -3,7 +3,7 @@
 // at load time by hipRTC (jit.cpp, model constants as compile-time immediates).
 #pragma once
 
-#include "spatial.hip.hpp"
+#include "tree_body.hip.hpp"
 
 namespace rbamd {
 namespace dev {
@@ -83,6 +83,15 @@ __device__ __forceinline__ void rnea_eval(const T *mdl, const T (&qv)[N], const 
     out(0, fn[0].z);
 }
 
+template <typename T, int N, bool FAST, typename Topo, typename Out>
+__device__ __forceinline__ void rnea_any(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&qddv)[N],
+                                         Out &&out) {
+    if constexpr (Topo::kSerial)
+        rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, static_cast<Out &&>(out));
+    else
+        rnea_eval_tree<T, N, FAST, Topo>(mdl, qv, qdv, qddv, static_cast<Out &&>(out));
+}
+
 template <typename T, int N>
 __device__ __forceinline__ void load_cfg(const T *__restrict__ a, const T *__restrict__ b,
                                          const T *__restrict__ c, int64_t ld, uint32_t off,
@@ -96,19 +105,19 @@ __device__ __forceinline__ void load_cfg(const T *__restrict__ a, const T *__res
 }
 
 // Lane bodies: `mdl` points at the packed model (LDS copy or a constexpr array).
-template <typename T, int N, bool FAST>
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void rnea_lane(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
                                           const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b,
                                           int64_t ld) {
     const uint32_t off = b * (uint32_t)sizeof(T);
     T qv[N], qdv[N], qddv[N];
     load_cfg<T, N>(q, qd, qdd, ld, off, qv, qdv, qddv);
-    rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
+    rnea_any<T, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
 }
 
 // Streaming form: walk the batch with `stride`, prefetching the next configuration's
 // joint values into registers before evaluating the current one.
-template <typename T, int N, bool FAST>
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void rnea_stream_lane(const T *mdl, const T *__restrict__ q,
                                                  const T *__restrict__ qd, const T *__restrict__ qdd,
                                                  T *__restrict__ tau, uint32_t b, uint32_t stride,
@@ -120,7 +129,7 @@ __device__ __forceinline__ void rnea_stream_lane(const T *mdl, const T *__restri
         T nq[N], nqd[N], nqdd[N];
         if (more) load_cfg<T, N>(q, qd, qdd, ld, bn * (uint32_t)sizeof(T), nq, nqd, nqdd);
         const uint32_t off = b * (uint32_t)sizeof(T);
-        rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
+        rnea_any<T, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
         if (!more) break;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -189,7 +198,7 @@ __device__ __forceinline__ void tile_store(T *__restrict__ dst, int64_t ld, uint
 
 // Whole-block tile: caller guarantees b0 + 256 <= B and 16-byte alignment of every row
 // start (base pointers and ld * sizeof(T) multiples of 16).  `tile` holds 3N rows.
-template <typename T, int N, bool FAST>
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void rnea_tile(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
                                           const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b0,
                                           int64_t ld, T *tile) {
@@ -204,7 +213,7 @@ __device__ __forceinline__ void rnea_tile(const T *mdl, const T *__restrict__ q,
         qddv[j] = tile[(2 * N + j) * kTile + t];
     }
     __syncthreads();  // every lane holds its inputs; rows 0..N-1 become the output tile
-    rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, [&](int j, T v) { tile[j * kTile + t] = v; });
+    rnea_any<T, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, T v) { tile[j * kTile + t] = v; });
     __syncthreads();
     tile_store<T, N>(tau, ld, b0, tile);
 }

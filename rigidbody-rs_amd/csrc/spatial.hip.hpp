@@ -111,6 +111,16 @@ __device__ __forceinline__ V3<T> mul_add(const V3<T> &acc, const S3<T> &S, const
               fmadd(S.xz, x.x, fmadd(S.yz, x.y, fmadd(S.zz, x.z, acc.z))));
 }
 
+// Topology of the reference's Multibody (multibody.rs:32): a serial chain of revolute
+// joints, parent(j) = j - 1.  The lane functions take a `Topo` policy; this one selects the
+// tuned serial code, a model-specialised kernel of a tree model gets its own (jit.cpp,
+// tree_body.hip.hpp).
+struct SerialTopo {
+    static constexpr bool kSerial = true;
+    static constexpr int parent(int j) { return j - 1; }
+    static constexpr bool prismatic(int) { return false; }
+};
+
 // Per-link model constants.  Each workgroup first copies the packed block (layout.hpp,
 // n * 24 scalars, <= 5.8 KB) from HBM/L2 into LDS (stage_model); every later read is a
 // wave-uniform LDS broadcast, issued where the link is processed.  (Reading the block

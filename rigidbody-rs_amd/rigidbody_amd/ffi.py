@@ -84,8 +84,10 @@ _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
 _sig("multibody_kernel_path", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int])
 _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
-KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3}
-GENERAL_AXES, URDF_TREE = 1, 2  # rigidbody_batch.h RB_MODEL_*
+KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3, "fwd_kin": 4, "jac": 5}
+GENERAL_AXES, URDF_TREE, FLOATING_BASE = 1, 2, 4  # rigidbody_batch.h RB_MODEL_*
+_ip = ctypes.POINTER(ctypes.c_int)
+_sig("multibody_topology", ctypes.c_int, [_vp, _ip, _ip])
 for _t in ("f32", "f64"):
     _sig(f"multibody_rollout_batch_{_t}", ctypes.c_int,
          [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_int, _vp, _i64, _i64, _vp])
@@ -204,7 +206,8 @@ class Multibody:
 
     @classmethod
     def from_urdf(cls, path, flags: int = 0):
-        """flags: GENERAL_AXES | URDF_TREE (rigidbody_batch.h RB_MODEL_*); 0 = the reference's reading."""
+        """flags: GENERAL_AXES | URDF_TREE | FLOATING_BASE (rigidbody_batch.h RB_MODEL_*); 0 = the
+        reference's reading."""
         if flags:
             return cls(_lib.multibody_new_from_urdf_ex(os.fsencode(path), flags))
         return cls(_lib.multibody_new_from_urdf(os.fsencode(path)))
@@ -254,6 +257,12 @@ class Multibody:
         arrs = [np.zeros(self.n) for _ in range(4)]
         _check(_lib.multibody_limits(self._h, *[a.ctypes.data_as(_dp) for a in arrs]), "limits")
         return tuple(arrs)  # lower, upper, velocity, effort
+
+    def topology(self):
+        """(parent [n] (-1 = base), joint_type [n] (0 revolute, 1 prismatic))."""
+        par, typ = np.zeros(self.n, dtype=np.int32), np.zeros(self.n, dtype=np.int32)
+        _check(_lib.multibody_topology(self._h, par.ctypes.data_as(_ip), typ.ctypes.data_as(_ip)), "topology")
+        return par, typ
 
     def upload(self):
         _check(_lib.multibody_upload(self._h), "upload")

@@ -71,7 +71,7 @@ def test_embedded_fr3_model(ffi):
 
 def _blob_links(blob):
     n = int(blob[2])
-    return n, blob[5:].reshape(n, 36)  # header: magic, version 2, n, pairing, flags
+    return n, blob[5:].reshape(n, 38)  # header: magic, version 3, n, pairing, flags
 
 
 def test_model_build_matches_oracle(ffi, fr3_text, oracle_mod):

@@ -68,7 +68,7 @@ def test_tree_reading_cpp_matches_python(n, oracle_mod):
     fr = _frames(xml)
     mb = ffi.Multibody.from_urdf_string(xml, ffi.GENERAL_AXES | ffi.URDF_TREE)
     assert mb.n == n and mb.flags == 3
-    L = mb.blob()[5:].reshape(n, 36)
+    L = mb.blob()[5:].reshape(n, 38)
     for i in range(n):
         R = oracle_mod.quat_to_matrix(L[i, 3:7])
         assert np.abs(R - fr["Rp"][i]).max() <= 1e-13
@@ -104,15 +104,17 @@ def test_model_flag_errors(oracle_mod):
     with pytest.raises(ffi.RigidBodyError, match="GENERAL_AXES"):
         ffi.Multibody.from_urdf_string(xml, ffi.URDF_TREE)
     with pytest.raises(ffi.RigidBodyError, match="flags"):
-        ffi.Multibody.from_urdf_string(xml, 4)
+        ffi.Multibody.from_urdf_string(xml, 8)
+    # branching and prismatic joints are read (tests/test_tree.py); mimic is not
     branch = xml.replace("</robot>", '  <link name="extra"/>\n  <joint name="jx" type="revolute">\n'
                          '    <parent link="body3"/>\n    <child link="extra"/>\n    <axis xyz="0 0 1"/>\n'
                          "  </joint>\n</robot>")
-    with pytest.raises(ffi.RigidBodyError, match="branching"):
-        ffi.Multibody.from_urdf_string(branch, 3)
+    mb = ffi.Multibody.from_urdf_string(branch, 3)
+    par, typ = mb.topology()
+    assert mb.n == 8 and list(par).count(2) == 2 and not typ.any()
     prism = xml.replace('name="j5" type="revolute"', 'name="j5" type="prismatic"')
-    with pytest.raises(ffi.RigidBodyError, match="prismatic"):
-        ffi.Multibody.from_urdf_string(prism, 3)
+    par, typ = ffi.Multibody.from_urdf_string(prism, 3).topology()
+    assert list(par) == list(range(-1, 6)) and list(typ) == [0, 0, 0, 0, 1, 0, 0]
     mimic = xml.replace('    <child link="body4"/>', '    <child link="body4"/>\n    <mimic joint="j3"/>')
     with pytest.raises(ffi.RigidBodyError, match="mimic"):
         ffi.Multibody.from_urdf_string(mimic, 3)
