@@ -98,9 +98,21 @@ def make_sets(mb, B, dtype, kernel, nsets, seed, pad=0, layout="soa"):
     layout "tiled": [ceil(B/256), n, 256] tensors (rigidbody_batch.h), filled with the
     same values as the SoA sets (device fill, then rb_to_tiled)."""
     if layout == "tiled":
+        # pad > 0 (tiled): array k of a set starts k * pad elements into its own buffer --
+        # staggers the arrays' base addresses (channel-aliasing experiments, tools/ab_bench.py)
+        def placed(t, k):
+            tt = ffi.to_tiled(t)
+            if not pad:
+                return tt
+            buf = torch.empty(k * pad + tt.numel(), dtype=tt.dtype, device=tt.device)
+            v = buf[k * pad:].view(tt.shape)
+            v.copy_(tt)
+            return v
+
         sets = []
         for ins, outs in make_sets(mb, B, dtype, kernel, nsets, seed):
-            sets.append(([ffi.to_tiled(t) for t in ins], [ffi.to_tiled(t) for t in outs]))
+            sets.append(([placed(t, k) for k, t in enumerate(ins)],
+                         [placed(t, len(ins) + k) for k, t in enumerate(outs)]))
             del ins, outs
         torch.cuda.synchronize()
         return sets
@@ -271,6 +283,11 @@ def side_workloads(mb7, a, rotate_gib):
     mb30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     mb30.upload()
     one("rnea_chain30_f32", mb30, "rnea", "f32")             # config 5
+    # a floating-base branching tree (6 virtual + 8 joints, 2 prismatic)
+    mbt = ffi.Multibody.from_urdf_string(chains.tree_urdf(floating=True), ffi.FLOATING_BASE)
+    mbt.upload()
+    one("rnea_float14_tree_f32", mbt, "rnea", "f32")
+    one("fd_float14_tree_f32", mbt, "fd", "f32")
     # fused rollout: K forward-dynamics + Euler steps per launch
     # (its clock settles only after ~150 ms of this VALU-dense load: 495 -> 357 us per launch)
     K, nl = 16, 40
