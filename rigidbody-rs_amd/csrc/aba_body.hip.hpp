@@ -156,11 +156,12 @@ __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, 
 }
 
 // Resident grid-stride form (A/B, model-specialised kernels): each lane walks the batch
-// with stride gridDim.x * 256 and issues the NEXT configuration's q, qd loads before
-// evaluating the current one (14 VGPRs in fp32 FR3); tau is loaded per configuration, its
-// latency hidden behind pass 1.  Block k of pass i covers configurations
-// (k + i * gridDim.x) * 256 + [0, 256); the tiled / SoA block base is o(b0) =
-// (b0 / 256) * bs + b0 % 256 as in the lane kernels.
+// with stride gridDim.x * 256 and issues the NEXT configuration's q, qd, tau loads before
+// evaluating the current one, so a block's loads for configuration k+1 are in flight while it
+// computes k (21 VGPRs in fp32 FR3).  The current set is always older than the prefetch in
+// the in-order vmcnt queue, so its counted waits never wait for the prefetch.  Block k of
+// pass i covers configurations (k + i * gridDim.x) * 256 + [0, 256); the tiled / SoA block
+// base is o(b0) = (b0 / 256) * bs + b0 % 256 as in the lane kernels.
 template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void aba_stream(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
                                            const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
@@ -169,29 +170,24 @@ __device__ __forceinline__ void aba_stream(const T *mdl, const T *__restrict__ q
     uint32_t blk = blockIdx.x;
     const uint32_t nblk = (B + 255u) / 256u;
     auto base = [&](uint32_t k) { return (int64_t)k * bs; };
-    T qv[N], qdv[N];
-    bool live = blk * 256u + threadIdx.x < B;
-    if (live) {
+    auto load = [&](uint32_t k, T (&x)[N], T (&y)[N], T (&z)[N]) {
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            qv[j] = ld_row(q + base(blk), j * ld, off);
-            qdv[j] = ld_row(qd + base(blk), j * ld, off);
+            x[j] = ld_row(q + base(k), j * ld, off);
+            y[j] = ld_row(qd + base(k), j * ld, off);
         }
-    }
+#pragma unroll
+        for (int j = N - 1; j >= 0; --j) z[j] = ld_row(tau + base(k), j * ld, off);
+    };
+    T qv[N], qdv[N], tv[N];
+    bool live = blk < nblk && blk * 256u + threadIdx.x < B;
+    if (live) load(blk, qv, qdv, tv);
     while (blk < nblk) {
         const uint32_t nxt = blk + gridDim.x;
         const bool nlive = nxt < nblk && nxt * 256u + threadIdx.x < B;
-        T nq[N], nqd[N], tv[N];
-        if (nlive) {
-#pragma unroll
-            for (int j = 0; j < N; ++j) {
-                nq[j] = ld_row(q + base(nxt), j * ld, off);
-                nqd[j] = ld_row(qd + base(nxt), j * ld, off);
-            }
-        }
+        T nq[N], nqd[N], nt[N];
+        if (nlive) load(nxt, nq, nqd, nt);
         if (live) {
-#pragma unroll
-            for (int j = 0; j < N; ++j) tv[j] = ld_row(tau + base(blk), j * ld, off);
             T *out = qdd + base(blk);
             aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(out, j * ld, off, v); });
         }
@@ -199,6 +195,7 @@ __device__ __forceinline__ void aba_stream(const T *mdl, const T *__restrict__ q
         for (int j = 0; j < N; ++j) {
             qv[j] = nq[j];
             qdv[j] = nqd[j];
+            tv[j] = nt[j];
         }
         live = nlive;
         blk = nxt;

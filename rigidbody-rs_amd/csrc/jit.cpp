@@ -52,7 +52,8 @@ int jit_nt(JitKind kind) {
 bool jit_opaque(JitKind kind, bool f64, int n) {
     const int v = tuning().opaque_consts;
     if (v >= 0) return v != 0;
-    return n <= 16 && (kind == JitKind::Rollout || (kind == JitKind::Fd && !f64));
+    (void)f64;
+    return n <= 16 && kind == JitKind::Rollout;
 }
 
 int jit_waves(JitKind kind, bool f64, int n) {

@@ -24,9 +24,10 @@ struct Tuning {
     // 129+ VGPRs, one wave per SIMD fewer; 361 vs 390 us for 16 FR3 steps).
     int jit_waves = -1;
     // Model constants pinned per use (spatial.hip.hpp mconst): 1 on, 0 off, -1 auto = the
-    // rollout (fp32 390 vs 512 us; fp64 810 vs 995 us) and fp32 forward dynamics (33.8 vs
-    // 35.7 us) of chains up to 16 links; off for fp64 forward dynamics (90 vs 71 us), for
-    // longer chains (30-link fp32 FD: 1331 vs 333 us) and for the other kinds.
+    // rollout of chains up to 16 links (fp32 337 vs 1736 us; fp64 810 vs 995 us); off for
+    // forward dynamics (fp32 29.6 vs 31.9 us once the 1/D reciprocal freed 12 VGPRs -- it
+    // was 33.8 vs 35.7 the other way before; fp64 71 vs 90 us; 30-link fp32 333 vs 1331 us)
+    // and for the other kinds.
     int opaque_consts = -1;
     // JIT forward dynamics: 1 = resident grid-stride form with register prefetch (aba_stream).
     int fd_stream = 0;

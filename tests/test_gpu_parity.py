@@ -372,3 +372,39 @@ def test_tiled_layout_matches_soa_bitwise(name, ffi, dev, fr3_text):
             mb.rnea_batch_tiled(xt[0][:, :, :128].contiguous(), xt[1], xt[2], 65536 + 3)
     finally:
         ffi.set_tuning("jit", 1)
+
+
+def test_single_config_abi_is_reentrant(dev):
+    """Concurrent single-configuration calls on one handle (SURVEY §8(b) threading: the
+    reference's queries take *const Multibody; each thread gets its own stream/staging)."""
+    import threading
+
+    from oracle import oracle, urdf_model
+    from rigidbody_amd import chains, ffi
+
+    mb = ffi.Multibody.new()
+    om = oracle.Model(urdf_model.model_raw_from_urdf(chains.fr3_urdf_text()))
+    rng = np.random.default_rng(17)
+    qs = rng.uniform(-2, 2, (8, 3, 7))
+    errs = []
+
+    def work(k):
+        try:
+            for _ in range(20):
+                q, qd, qdd = qs[k]
+                got = mb.rnea(q, qd, qdd)
+                ref = om.rnea(q, qd, qdd)
+                if np.abs(got - ref).max() > 1e-9 * (1 + np.abs(ref).max()):
+                    errs.append((k, np.abs(got - ref).max()))
+                H = mb.crba_raw(q)
+                if np.abs(H - om.crba_raw(q)).max() > 1e-9 * (1 + np.abs(H).max()):
+                    errs.append((k, "crba"))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append((k, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
