@@ -155,6 +155,29 @@ __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, 
     aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
 }
 
+// Paired lane (fp32 model-specialised kernels, spatial.hip.hpp f2): the configurations at
+// lane offset `off` of the batch blocks starting at elements oA and oB; loads in the same
+// first-use order as aba_lane.
+template <int N, bool FAST, typename Topo = SerialTopo>
+__device__ __forceinline__ void aba_lane2(const f2 *mdl, const float *__restrict__ q, const float *__restrict__ qd,
+                                          const float *__restrict__ tau, float *__restrict__ qdd, int64_t oA,
+                                          int64_t oB, uint32_t off, int64_t ld) {
+    f2 qv[N], qdv[N], tv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qv[j] = ld_row2(q, oA, oB, j * ld, off);
+        __builtin_amdgcn_sched_barrier(0);
+        qdv[j] = ld_row2(qd, oA, oB, j * ld, off);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) {
+        tv[j] = ld_row2(tau, oA, oB, j * ld, off);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 v) { st_row2(qdd, oA, oB, j * ld, off, v); });
+}
+
 // Resident grid-stride form (A/B, model-specialised kernels): each lane walks the batch
 // with stride gridDim.x * 256 and issues the NEXT configuration's q, qd, tau loads before
 // evaluating the current one, so a block's loads for configuration k+1 are in flight while it

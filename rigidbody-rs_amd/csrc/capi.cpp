@@ -151,18 +151,21 @@ bool jit_stream(rbamd::JitKind kind, bool f64, int n) {
 
 // The hipRTC kernel of `kind` for this model on the current device, or nullptr (the
 // precompiled generic kernel then runs).
-const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f64, bool fast) {
+// pack: configurations per lane, 0 = the jit_pack policy (jit.cpp).
+const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f64, bool fast, int pack = 0) {
     if (!rbamd::jit_enabled()) return nullptr;
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
     const bool stream = jit_stream(kind, f64, mb->model.n);
     const bool fst = fast && !f64;
+    if (pack <= 0) pack = rbamd::jit_pack(kind, f64, mb->model.n, stream);
     const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
-                            (fst ? ":fast" : ":precise") + (stream ? ":stream" : ":lane") + rbamd::jit_tag(kind, f64, mb->model.n);
+                            (fst ? ":fast" : ":precise") + (stream ? ":stream" : ":lane") +
+                            rbamd::jit_tag(kind, f64, mb->model.n) + ":q" + std::to_string(pack);
     std::lock_guard<std::mutex> lk(mb->mu);
     auto it = mb->jit.find(key);
     if (it == mb->jit.end()) {
-        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, stream)).first;
+        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, stream, pack)).first;
         mb->jit_device[key] = d;
     }
     return it->second.function ? &it->second : nullptr;
@@ -187,8 +190,13 @@ hipError_t no_generic(const Multibody *mb) {
     return hipErrorNotSupported;
 }
 
+// Smallest batch for which the auto policy takes the paired-lane kernel: one resident round
+// of it (2 blocks of 512 configurations per CU x 256 CUs) -- 2^18.
+constexpr uint32_t kPackMinBatch = 1u << 18;
+
 hipError_t jit_launch(const rbamd::JitKernel *jk, hipFunction_t fn, uint32_t B, void **args, hipStream_t s) {
-    const unsigned full = (B + 255u) / 256u;
+    const unsigned per_block = 256u * (unsigned)jk->pack;
+    const unsigned full = (unsigned)(((uint64_t)B + per_block - 1) / per_block);
     unsigned g = full;
     if (jk->stream) {
         const int f = rbamd::tuning().grid_factor < 1 ? 1 : rbamd::tuning().grid_factor;
@@ -223,7 +231,10 @@ template <typename T>
 hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *tau, T *qdd,
                          uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Fd, sizeof(T) == 8, fast_trig())) {
+    // Paired lanes (jit_pack) halve the grid: below kPackMinBatch the one-per-lane kernel
+    // fills more CUs and wins (FR3 fp32 65536: 4.7 vs 5.2 us; 2^20: 31.0 vs 29.2 us).
+    const int pack = (rbamd::tuning().pack < 0 && B < kPackMinBatch) ? 1 : 0;
+    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Fd, sizeof(T) == 8, fast_trig(), pack)) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau, (void *)&qdd, (void *)&B, (void *)&lda, (void *)&bs};
         return jit_launch(jk, jk->function, B, args, s);
@@ -762,6 +773,7 @@ int rb_set_tuning(const char *key, int value) {
     else if (k == "jit_variant") t.jit_variant = value;
     else if (k == "opaque_consts") t.opaque_consts = value;
     else if (k == "fd_stream") t.fd_stream = value;
+    else if (k == "pack") t.pack = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

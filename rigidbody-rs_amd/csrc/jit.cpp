@@ -62,12 +62,26 @@ int jit_waves(JitKind kind, bool f64, int n) {
     return (kind == JitKind::Rollout && !f64 && n <= 8) ? 4 : 0;
 }
 
-std::string jit_tag(JitKind kind, bool f64, int n) {
-    return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
-           std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":v" + std::to_string(tuning().jit_variant);
+int jit_pack(JitKind kind, bool f64, int n, bool stream) {
+    // The rollout is not paired: with its K loop around the dynamics the pair needs 256 VGPRs
+    // (1 wave/SIMD) unpinned, or spills at 2-4 waves with pinned constants.
+    if (f64 || stream || (kind != JitKind::Rnea && kind != JitKind::Fd)) return 1;
+    const int v = tuning().pack;
+    if (v >= 0) return v >= 2 ? 2 : 1;
+    // Auto: forward dynamics of chains up to 8 links (FR3 fp32 2^20 tiled: 28.7 vs 30.7 us;
+    // 200 VGPRs for the pair, 2 waves/SIMD).  RNEA stays one per lane: its pair needs 128
+    // VGPRs (4 waves/SIMD instead of 8) and measured slower, 22.6 vs 21.0 us, although it
+    // issues half the VALU work.  The 30-link chain needs ~240 VGPRs for one configuration.
+    return (kind == JitKind::Fd && n <= 8) ? 2 : 1;
 }
 
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream) {
+std::string jit_tag(JitKind kind, bool f64, int n) {
+    return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
+           std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n, false)) +
+           ":v" + std::to_string(tuning().jit_variant);
+}
+
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack_req) {
     std::vector<double> pk = m.pack_f64();
     for (int i = 0; i < m.n; ++i) {
         double *c = &pk[(size_t)i * kLinkStride];
@@ -75,6 +89,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         for (int k = 0; k < 3; ++k) c[kP + k] = snap(c[kP + k]);
     }
     const char *F = fast ? "true" : "false";
+    const int pack = pack_req > 0 ? pack_req : jit_pack(kind, f64, m.n, stream);
     std::ostringstream o;
     o << "#define RB_NT " << jit_nt(kind) << "\n";
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
@@ -103,9 +118,26 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
              "  static constexpr bool on_path(int j) { return j == N - 1 || is_ancestor(j, N - 1); }\n"
              "};\n";
     }
-    o << "static __device__ constexpr T kModel[" << pk.size() << "] = {\n";
-    for (size_t k = 0; k < pk.size(); ++k) o << "  " << literal(pk[k], f64) << ",\n";
+    if (pack == 2) {  // paired fp32 lanes: every constant splat to both halves (spatial.hip.hpp f2)
+        o << "using TV = rbamd::dev::f2;\n";
+        o << "static __device__ constexpr TV kModel[" << pk.size() << "] = {\n";
+        for (size_t k = 0; k < pk.size(); ++k) {
+            const std::string c = literal(pk[k], f64);
+            o << "  TV{" << c << ", " << c << "},\n";
+        }
+    } else {
+        o << "static __device__ constexpr T kModel[" << pk.size() << "] = {\n";
+        for (size_t k = 0; k < pk.size(); ++k) o << "  " << literal(pk[k], f64) << ",\n";
+    }
     o << "};\n";
+    // Paired lanes: block k owns batch blocks 2k and 2k+1 (SoA: configurations 512k + t and
+    // 512k + 256 + t; tiled: lane t of tiles 2k and 2k+1).  When the second is past B, the
+    // lane evaluates the first twice and stores the bit-identical value twice.
+    const char *pair_prologue =
+        "  const uint32_t bA = blockIdx.x * 512u + threadIdx.x;\n"
+        "  if (bA >= B) return;\n"
+        "  const int64_t oA = (int64_t)(2u * blockIdx.x) * bs;\n"
+        "  const int64_t oB = bA + 256u < B ? oA + bs : oA;\n";
     std::string head_s = "extern \"C\" __global__ __launch_bounds__(256) ";
     if (const int w = jit_waves(kind, f64, m.n))
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
@@ -118,7 +150,11 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
-        if (stream) {  // SoA only (capi.cpp)
+        if (pack == 2) {
+            o << pair_prologue;
+            o << "  rbamd::dev::rnea_lane2<N, " << F
+              << ", Topo>(kModel, q, qd, qdd, tau, oA, oB, threadIdx.x * 4u, ld);\n";
+        } else if (stream) {  // SoA only (capi.cpp)
             o << "  T qv[N], qdv[N], qddv[N];\n";
             o << "  rbamd::dev::load_cfg<T, N>(q, qd, qdd, ld, b * (uint32_t)sizeof(T), qv, qdv, qddv);\n";
             o << "  rbamd::dev::rnea_stream_lane<T, N, " << F
@@ -128,7 +164,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
             o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
         }
         o << "}\n";
-        if (jit_tile_ok(m.n, f64)) {  // SoA only
+        if (pack == 1 && jit_tile_ok(m.n, f64)) {  // SoA only
             o << head << "rb_jit_tile(const T *__restrict__ q, const T *__restrict__ qd, "
                  "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
             o << "  __shared__ T tile[3 * N * 256];\n";
@@ -143,7 +179,11 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
-        if (stream) {
+        if (pack == 2) {
+            o << pair_prologue;
+            o << "  rbamd::dev::aba_lane2<N, " << F
+              << ", Topo>(kModel, q, qd, tau, qdd, oA, oB, threadIdx.x * 4u, ld);\n}\n";
+        } else if (stream) {
             o << "  rbamd::dev::aba_stream<T, N, " << F << ", Topo>(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
         } else {
             o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
@@ -174,8 +214,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
 }
 
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream, const std::string &arch,
-                 std::vector<char> *code, std::string *error) {
-    const std::string src = jit_source(m, kind, f64, fast, stream);
+                 std::vector<char> *code, std::string *error, int pack) {
+    const std::string src = jit_source(m, kind, f64, fast, stream, pack);
     hiprtcProgram prog = nullptr;
     if (hiprtcCreateProgram(&prog, src.c_str(), "rb_jit.hip", kJitHeaderCount, kJitHeaderSources,
                             kJitHeaderNames) != HIPRTC_SUCCESS) {
@@ -202,9 +242,10 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream,
     return true;
 }
 
-JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stream) {
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack) {
     JitKernel jk;
     jk.stream = stream;
+    jk.pack = pack > 0 ? pack : jit_pack(kind, f64, m.n, stream);
     int dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
@@ -212,14 +253,14 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stre
         return jk;
     }
     std::vector<char> code;
-    if (!jit_compile(m, kind, f64, fast, stream, prop.gcnArchName, &code, &jk.error)) return jk;
+    if (!jit_compile(m, kind, f64, fast, stream, prop.gcnArchName, &code, &jk.error, jk.pack)) return jk;
     hipError_t e = hipModuleLoadData(&jk.module, code.data());
     if (e != hipSuccess) {
         jk.error = std::string("hipModuleLoadData: ") + hipGetErrorString(e);
         jk.module = nullptr;
         return jk;
     }
-    if (kind == JitKind::Rnea && jit_tile_ok(m.n, f64) &&
+    if (kind == JitKind::Rnea && jk.pack == 1 && jit_tile_ok(m.n, f64) &&
         hipModuleGetFunction(&jk.tile_function, jk.module, "rb_jit_tile") != hipSuccess)
         jk.tile_function = nullptr;
     e = hipModuleGetFunction(&jk.function, jk.module, "rb_jit_kernel");

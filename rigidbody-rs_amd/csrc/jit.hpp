@@ -32,6 +32,7 @@ struct JitKernel {
     hipFunction_t function = nullptr;       // one configuration per lane (any layout)
     hipFunction_t tile_function = nullptr;  // LDS-tiled, 16-byte global accesses (aligned SoA)
     bool stream = false;        // grid-stride form: launch a resident-sized grid
+    int pack = 1;               // configurations per lane (2: paired fp32 lanes, 512 per block)
     unsigned resident = 0;      // resident blocks (occupancy x CUs) for the stream form
     std::string error;          // non-empty when compilation failed
 };
@@ -42,20 +43,23 @@ bool jit_enabled();
 bool jit_tile_ok(int n, bool f64);
 
 // Generated HIP source for one specialised kernel (exposed for tests / inspection).
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream);
+// pack: configurations per lane, 0 = the jit_pack policy.
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack = 0);
 
 // Non-temporal access bits of `kind`'s JIT source, and the cache-key suffix of every
 // tuning value that changes the source (tuning.hpp).
 int jit_nt(JitKind kind);
 bool jit_opaque(JitKind kind, bool f64, int n);
 int jit_waves(JitKind kind, bool f64, int n);
+// Configurations per lane of `kind`'s lane kernel (tuning `pack`): 2 = paired fp32 lanes.
+int jit_pack(JitKind kind, bool f64, int n, bool stream);
 std::string jit_tag(JitKind kind, bool f64, int n);
 
 // hipRTC compilation only (no device needed): fills `code` with the code object.
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream, const std::string &arch,
-                 std::vector<char> *code, std::string *error);
+                 std::vector<char> *code, std::string *error, int pack = 0);
 
 // Compiles and loads the kernel on the current device.  Never throws.
-JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stream);
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack = 0);
 
 }  // namespace rbamd

@@ -115,6 +115,22 @@ __device__ __forceinline__ void rnea_lane(const T *mdl, const T *__restrict__ q,
     rnea_any<T, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
 }
 
+// Paired lane (fp32 model-specialised kernels, spatial.hip.hpp f2): the configurations at
+// lane offset `off` of the batch blocks starting at elements oA and oB, evaluated together.
+template <int N, bool FAST, typename Topo = SerialTopo>
+__device__ __forceinline__ void rnea_lane2(const f2 *mdl, const float *__restrict__ q, const float *__restrict__ qd,
+                                           const float *__restrict__ qdd, float *__restrict__ tau, int64_t oA,
+                                           int64_t oB, uint32_t off, int64_t ld) {
+    f2 qv[N], qdv[N], qddv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qv[j] = ld_row2(q, oA, oB, j * ld, off);
+        qdv[j] = ld_row2(qd, oA, oB, j * ld, off);
+        qddv[j] = ld_row2(qdd, oA, oB, j * ld, off);
+    }
+    rnea_any<f2, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, f2 v) { st_row2(tau, oA, oB, j * ld, off, v); });
+}
+
 // Streaming form: walk the batch with `stride`, prefetching the next configuration's
 // joint values into registers before evaluating the current one.
 template <typename T, int N, bool FAST, typename Topo = SerialTopo>

@@ -33,6 +33,16 @@ namespace dev {
 __device__ __forceinline__ float fmadd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ double fmadd(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// Paired fp32 lanes (model-specialised fp32 kernels, tuning `pack`): a lane evaluates two
+// configurations at once as a 2-wide vector, so every FMA/MUL/ADD of the recursion becomes
+// one v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (FR3 RNEA: 646 VALU instructions per PAIR
+// vs 586 per configuration).  gfx950 already issues a wave64 v_fma_f32 in 2 cycles, so this
+// is not a throughput doubling; what pays is the second independent dependency chain per
+// lane for the latency-bound forward dynamics (FR3: 28.7 vs 30.7 us).  Only
+// sin/cos and 1/x stay per element; both halves run identical instruction sequences.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fmadd(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 template <typename T>
 struct V3 {
     T x, y, z;
@@ -183,6 +193,7 @@ __device__ __forceinline__ T mconst(T v) {
     }
     return v;
 }
+__device__ __forceinline__ f2 mconst(f2 v) { return v; }  // paired kernels do not pin constants
 
 template <typename T>
 __device__ __forceinline__ Link<T> load_link(const T *__restrict__ mdl, int i) {
@@ -339,6 +350,14 @@ template <bool FAST>
 __device__ __forceinline__ void sin_cos(double x, double &s, double &c) {
     sincos_cw(x, s, c);
 }
+template <bool FAST>
+__device__ __forceinline__ void sin_cos(f2 x, f2 &s, f2 &c) {
+    float s0, c0, s1, c1;
+    sin_cos<FAST>(x.x, s0, c0);
+    sin_cos<FAST>(x.y, s1, c1);
+    s = f2{s0, s1};
+    c = f2{c0, c1};
+}
 
 // 1/x for the ABA's joint-space inertia D > 0 (normal range).  The IEEE division the
 // compiler emits is ~10 instructions (div_scale x2, rcp, 4 FMAs, div_fmas, div_fixup);
@@ -349,6 +368,20 @@ __device__ __forceinline__ double recip(double x) {
     double r = __builtin_amdgcn_rcp(x);
     r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
     return __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ f2 recip(f2 x) { return f2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; }
+
+// Paired-lane row access: one configuration from each of two batch blocks (base offsets oA,
+// oB in elements, the same lane byte offset), so each half's loads/stores stay fully
+// coalesced dword rows in either layout.
+__device__ __forceinline__ f2 ld_row2(const float *__restrict__ base, int64_t oA, int64_t oB, int64_t row,
+                                      uint32_t off) {
+    return f2{ld_row(base + oA, row, off), ld_row(base + oB, row, off)};
+}
+__device__ __forceinline__ void st_row2(float *__restrict__ base, int64_t oA, int64_t oB, int64_t row, uint32_t off,
+                                        f2 v) {
+    st_row(base + oA, row, off, v.x);
+    st_row(base + oB, row, off, v.y);
 }
 
 }  // namespace dev

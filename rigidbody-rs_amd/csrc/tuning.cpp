@@ -30,6 +30,7 @@ Tuning &tuning() {
         x.fd_stream = env_int("RB_FD_STREAM", x.fd_stream);
         x.jit_waves = env_int("RB_JIT_WAVES", x.jit_waves);
         x.jit_variant = env_int("RB_JIT_VARIANT", x.jit_variant);
+        x.pack = env_int("RB_PACK", x.pack);
         return x;
     }();
     return t;

@@ -31,6 +31,10 @@ struct Tuning {
     int opaque_consts = -1;
     // JIT forward dynamics: 1 = resident grid-stride form with register prefetch (aba_stream).
     int fd_stream = 0;
+    // JIT fp32 RNEA / forward dynamics: 1 = two configurations per lane on packed fp32
+    // (spatial.hip.hpp f2; 512 configurations per 256-lane block), 0 = one per lane,
+    // -1 auto (jit_pack in jit.cpp).
+    int pack = -1;
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
     int jit_variant = 0;
 };

@@ -408,3 +408,43 @@ def test_single_config_abi_is_reentrant(dev):
     for t in ts:
         t.join()
     assert not errs, errs
+
+
+@pytest.mark.parametrize("kind", ["rnea", "fd"])
+def test_paired_lane_kernels(kind, ffi, dev, fr3_text):
+    """fp32 model-specialised kernels with two configurations per lane on packed fp32
+    (tuning `pack`, the default for chains up to 8 links) against the one-per-lane form and
+    the oracle: ragged batches (second configuration of a lane past B, an odd number of
+    256-configuration tiles), SoA and tiled.  rnea: 1e-4 * (1 + |tau|) against the fp64
+    oracle on the fp32-rounded inputs; fd: torque residual 1e-3 * (1 + |tau|)."""
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    om = _oracle(fr3_text)
+    n = mb.n
+    outs = {}
+    try:
+        for pack in (1, 2):
+            ffi.set_tuning("pack", pack)
+            assert mb.kernel_path(kind, False) == "jit"
+            for B in (1, 255, 256, 257, 511, 513, 767, 65536 + 3):
+                rng = np.random.default_rng(B)
+                x = [_t(rng.uniform(-2, 2, (n, B)), dev, torch.float32) for _ in range(3)]
+                f = mb.rnea_batch if kind == "rnea" else mb.fd_batch
+                ft = mb.rnea_batch_tiled if kind == "rnea" else mb.fd_batch_tiled
+                outs[(pack, B, "soa")] = (x, f(*x))
+                xt = [ffi.to_tiled(a) for a in x]
+                outs[(pack, B, "tiled")] = (x, ffi.from_tiled(ft(*xt, B), B))
+    finally:
+        ffi.set_tuning("pack", -1)
+    for (pack, B, lay), (x, v) in outs.items():
+        assert torch.isfinite(v).all(), (pack, B, lay)
+        xs = [a.double().cpu().numpy() for a in x]
+        cols = np.unique(np.r_[np.arange(min(B, 600)), np.arange(max(0, B - 600), B)])
+        xs = [a[:, cols] for a in xs]
+        got = v.double().cpu().numpy()[:, cols]
+        if kind == "rnea":
+            _close(got, om.rnea_batch(*xs), 1e-4, f"rnea pack={pack} B={B} {lay}")
+        else:
+            res = om.rnea_batch(xs[0], xs[1], got) - xs[2]
+            assert (np.abs(res) / (1 + np.abs(xs[2]))).max() <= 1e-3, (pack, B, lay)
+        if pack == 2:  # layouts agree bit for bit within one kernel form
+            assert torch.equal(v, outs[(2, B, "soa" if lay == "tiled" else "tiled")][1])
