@@ -267,7 +267,7 @@ def side_workloads(mb7, a, rotate_gib):
         per = set_bytes(mb.n, B, es, kernel)
         sets = make_sets(mb, B, ds, kernel, max(2, int(np.ceil(rotate_gib * (1 << 30) / per))), chains.SEED + 31,
                          layout=a.layout)
-        w, km = run_timed(mb, sets, kernel, ds, steps, 5, 1, 100.0, 1, a.layout, B)
+        w, km = run_timed(mb, sets, kernel, ds, steps, 5, 1, 300.0, 1, a.layout, B)
         sec[name] = {"evals_per_s": B * steps / w, "kernel_ms_avg": km, "batch": B, "layout": a.layout,
                      "hbm_frac": per / (km * 1e-3) / HBM_PEAK,
                      "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64") for k in kernel.split("_"))}

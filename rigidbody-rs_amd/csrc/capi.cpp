@@ -774,6 +774,7 @@ int rb_set_tuning(const char *key, int value) {
     else if (k == "opaque_consts") t.opaque_consts = value;
     else if (k == "fd_stream") t.fd_stream = value;
     else if (k == "pack") t.pack = value;
+    else if (k == "f64_tab") t.f64_tab = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

@@ -75,10 +75,12 @@ int jit_pack(JitKind kind, bool f64, int n, bool stream) {
     return (kind == JitKind::Fd && n <= 8) ? 2 : 1;
 }
 
+bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
+
 std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n, false)) +
-           ":v" + std::to_string(tuning().jit_variant);
+           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":v" + std::to_string(tuning().jit_variant);
 }
 
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack_req) {
@@ -94,6 +96,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     o << "#define RB_NT " << jit_nt(kind) << "\n";
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
     o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
+    const bool tab = jit_f64_tab(f64);
+    o << "#define RB_SINCOS_TAB " << (tab ? 1 : 0) << "\n";
     o << (kind == JitKind::Rnea                               ? "#include \"rnea_body.hip.hpp\"\n"
           : (kind == JitKind::Fd || kind == JitKind::Rollout) ? "#include \"aba_body.hip.hpp\"\n"
           : kind == JitKind::Crba                             ? "#include \"crba_body.hip.hpp\"\n"
@@ -210,7 +214,16 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         o << "  if (b >= B) return;\n";
         o << "  rbamd::dev::crba_lane<T, N, " << F << ", Topo>(kModel, q, H, b, ld);\n}\n";
     }
-    return o.str();
+    std::string src = o.str();
+    if (tab) {  // every kernel fills the block's sincos table first (all lanes still present)
+        for (const char *name : {"rb_jit_kernel(", "rb_jit_tile("}) {
+            const size_t at = src.find(name);
+            if (at == std::string::npos) continue;
+            const size_t body = src.find(") {\n", at);
+            if (body != std::string::npos) src.insert(body + 4, "  rbamd::dev::sctab_init();\n");
+        }
+    }
+    return src;
 }
 
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream, const std::string &arch,

@@ -346,9 +346,59 @@ __device__ __forceinline__ void sin_cos(float x, float &s, float &c) {
         sincos_cw(x, s, c);
     }
 }
+// Table-assisted fp64 sincos for the model-specialised fp64 kernels (RB_SINCOS_TAB, set by
+// jit.cpp): x = k pi/32 + r with |r| <= pi/64, (cos, sin)(k pi/32) from a 64-entry LDS table
+// the block fills once (sctab_init, wave 0 only), then degree-9/8 Taylor polynomials on r
+// (truncation < 1e-19) and one angle-addition step: ~22 VALU instructions per angle instead
+// of ~45 for sincos_cw's degree-13/14 minimax after a pi/2 reduction.  Entries come from
+// sincos_cw (<= 1 ulp), the result is within a few ulp of sin/cos(x).
+#ifndef RB_SINCOS_TAB
+#define RB_SINCOS_TAB 0
+#endif
+#if RB_SINCOS_TAB
+struct alignas(16) SinCosEntry {
+    double c, s;
+};
+__shared__ SinCosEntry rb_sctab[64];
+
+// Every wave of the block must call this before any sin_cos(double) (it ends in a barrier).
+__device__ __forceinline__ void sctab_init() {
+    if (threadIdx.x < 64) {
+        // pi/32 = (pi/2 split of sincos_cw) / 16, exact power-of-two scaling
+        const double a = __builtin_fma((double)threadIdx.x, 9.81747704246810386e-02,
+                                       (double)threadIdx.x * 3.82702124733547877e-18);
+        double s, c;
+        sincos_cw(a, s, c);
+        rb_sctab[threadIdx.x] = SinCosEntry{c, s};
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void sincos_tab(double x, double &s, double &c) {
+    const double k = __builtin_rint(x * 1.01859163578813017e+01);  // 32/pi
+    double r = __builtin_fma(-k, 9.81747704246810386e-02, x);      // pi/32 hi (pi/2 hi / 16)
+    r = __builtin_fma(-k, 3.82702124733547877e-18, r);              // pi/32 mid
+    r = __builtin_fma(-k, -9.35865565536981143e-35, r);             // pi/32 lo
+    const SinCosEntry e = rb_sctab[(int)k & 63];
+    const double z = r * r;
+    const double sr = __builtin_fma(r * z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+                          2.75573192239858907e-06, -1.98412698412698413e-04), 8.33333333333333322e-03),
+                          -1.66666666666666657e-01), r);
+    const double cr = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
+                          2.48015873015873016e-05, -1.38888888888888894e-03), 4.16666666666666644e-02),
+                          -0.5), 1.0);
+    s = __builtin_fma(e.s, cr, e.c * sr);
+    c = __builtin_fma(e.c, cr, -(e.s * sr));
+}
+#endif
+
 template <bool FAST>
 __device__ __forceinline__ void sin_cos(double x, double &s, double &c) {
+#if RB_SINCOS_TAB
+    sincos_tab(x, s, c);
+#else
     sincos_cw(x, s, c);
+#endif
 }
 template <bool FAST>
 __device__ __forceinline__ void sin_cos(f2 x, f2 &s, f2 &c) {

@@ -31,6 +31,7 @@ Tuning &tuning() {
         x.jit_waves = env_int("RB_JIT_WAVES", x.jit_waves);
         x.jit_variant = env_int("RB_JIT_VARIANT", x.jit_variant);
         x.pack = env_int("RB_PACK", x.pack);
+        x.f64_tab = env_int("RB_F64_TAB", x.f64_tab);
         return x;
     }();
     return t;

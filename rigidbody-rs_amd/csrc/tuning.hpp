@@ -35,6 +35,9 @@ struct Tuning {
     // (spatial.hip.hpp f2; 512 configurations per 256-lane block), 0 = one per lane,
     // -1 auto (jit_pack in jit.cpp).
     int pack = -1;
+    // JIT fp64 kernels: 1 = table-assisted sincos (spatial.hip.hpp sincos_tab), 0 = the
+    // pi/2-reduction minimax sincos_cw, -1 auto (on).
+    int f64_tab = -1;
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
     int jit_variant = 0;
 };
