@@ -775,6 +775,7 @@ int rb_set_tuning(const char *key, int value) {
     else if (k == "fd_stream") t.fd_stream = value;
     else if (k == "pack") t.pack = value;
     else if (k == "f64_tab") t.f64_tab = value;
+    else if (k == "rnea_seg") t.rnea_seg = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

@@ -77,10 +77,19 @@ int jit_pack(JitKind kind, bool f64, int n, bool stream) {
 
 bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
 
+// Segments of the RNEA lane kernel (rnea_eval_seg) for a serial chain of n links; 1 = one pass.
+int jit_rnea_seg(const Model &m, bool f64) {
+    (void)f64;
+    if (!m.serial_revolute()) return 1;
+    const int v = tuning().rnea_seg;
+    if (v >= 0) return v < 1 ? 1 : (v > m.n ? m.n : v);
+    return 1;
+}
+
 std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n, false)) +
-           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":v" + std::to_string(tuning().jit_variant);
+           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":s" + std::to_string(tuning().rnea_seg) + ":v" + std::to_string(tuning().jit_variant);
 }
 
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack_req) {
@@ -165,7 +174,11 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
               << ", Topo>(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
         } else {
             o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
-            o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
+            if (const int S = jit_rnea_seg(m, f64); S > 1)
+                o << "  rbamd::dev::rnea_lane_seg<T, N, " << S << ", " << F
+                  << ">(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
+            else
+                o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
         }
         o << "}\n";
         if (pack == 1 && jit_tile_ok(m.n, f64)) {  // SoA only

@@ -9,6 +9,77 @@ namespace rbamd {
 namespace dev {
 
 // ----------------------------------------------------------------------------- RNEA
+// Per-link steps of the serial-chain RNEA, shared by the one-pass form (rnea_eval) and the
+// segmented form (rnea_eval_seg) so both run the identical operation sequence.
+template <typename T>
+struct RneaState {
+    V3<T> w, v, aw, av;  // link velocity / acceleration (rot, lin), link coordinates
+};
+
+// Link 0: v_{-1} = 0, a_{-1} = (0, (0,0,+g)) -- multibody.rs:116-120
+template <typename T, bool FAST>
+__device__ __forceinline__ void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn, T &cs,
+                                          V3<T> &fn, V3<T> &ff) {
+    const Link<T> L = load_link(mdl, 0);
+    sin_cos<FAST>(q0, sn, cs);
+    const M3<T> E = joint_rotation(L.Rp, cs, sn);
+    const T g = T(kGravity);
+    st.w = v3(T(0), T(0), qd0);
+    st.v = v3(T(0), T(0), T(0));
+    st.aw = v3(T(0), T(0), qdd0);
+    st.av = v3(g * E.m[6], g * E.m[7], g * E.m[8]);  // E^T (0,0,g)
+    // I v with v = (w, 0):  n = I_o w,  f = -h x w
+    const V3<T> In = v3(L.Io.xz * qd0, L.Io.yz * qd0, L.Io.zz * qd0);
+    const V3<T> If = v3(-L.h.y * qd0, L.h.x * qd0, T(0));  // -h x (0,0,qd)
+    V3<T> An, Af;
+    inertia_mul(L, st.aw, st.av, An, Af);
+    ff = cross_add(Af, st.w, If);
+    fn = cross_add(An, st.w, In);
+}
+
+// Link j >= 1: forward sweep step (multibody.rs:122-141).
+template <typename T, bool FAST>
+__device__ __forceinline__ void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, T &sn, T &cs,
+                                         V3<T> &fn, V3<T> &ff) {
+    const Link<T> L = load_link(mdl, j);
+    sin_cos<FAST>(qj, sn, cs);
+    const M3<T> E = joint_rotation(L.Rp, cs, sn);
+    // SpatialVelocity::transform (spatial.rs:110-116) on v and a
+    const V3<T> u = cross_sub(st.v, L.p, st.w);
+    const V3<T> ua = cross_sub(st.av, L.p, st.aw);
+    V3<T> wn = mul_t(E, st.w), vn = mul_t(E, u);
+    V3<T> awn = mul_t(E, st.aw), avn = mul_t(E, ua);
+    wn.z += qdj;        // multibody.rs:130
+    awn.z += qddj;      // multibody.rs:133
+    avn.x = fmadd(vn.y, qdj, avn.x);   // multibody.rs:135-138, v x (z qd) unrolled
+    avn.y = fmadd(-vn.x, qdj, avn.y);
+    awn.x = fmadd(wn.y, qdj, awn.x);
+    awn.y = fmadd(-wn.x, qdj, awn.y);
+    st.w = wn; st.v = vn; st.aw = awn; st.av = avn;
+    // f = I a + v x* (I v)   (multibody.rs:140)
+    V3<T> In, If, An, Af;
+    inertia_mul(L, st.w, st.v, In, If);
+    inertia_mul(L, st.aw, st.av, An, Af);
+    ff = cross_add(Af, st.w, If);
+    fn = cross_add(cross_add(An, st.w, In), st.v, If);
+}
+
+// Backward sweep step: f_{j-1} += X_j^-1 f_j  (multibody.rs:145-150).
+template <typename T>
+__device__ __forceinline__ void rnea_bwd(const T *mdl, int j, T cj, T sj, const V3<T> &ffj, const V3<T> &fnj,
+                                         V3<T> &ffp, V3<T> &fnp) {
+    const T *c = mdl + j * kLinkStride;
+    const M3<T> Rp{{c[kE0 + 0], c[kE0 + 1], c[kE0 + 2], c[kE0 + 3], c[kE0 + 4], c[kE0 + 5],
+                    c[kE0 + 6], c[kE0 + 7], c[kE0 + 8]}};
+    const V3<T> p = v3(c[kP + 0], c[kP + 1], c[kP + 2]);
+    // E x = R_p (Rz x)
+    const V3<T> zf = v3(fmadd(cj, ffj.x, -sj * ffj.y), fmadd(sj, ffj.x, cj * ffj.y), ffj.z);
+    const V3<T> zn = v3(fmadd(cj, fnj.x, -sj * fnj.y), fmadd(sj, fnj.x, cj * fnj.y), fnj.z);
+    const V3<T> fl = mul(Rp, zf);
+    ffp = v3(ffp.x + fl.x, ffp.y + fl.y, ffp.z + fl.z);
+    fnp = cross_add(mul_add(fnp, Rp, zn), p, fl);
+}
+
 // Forward sweep (multibody.rs:122-141) then backward sweep (143-150), fused: the
 // per-link forces never leave registers.  One call evaluates the configuration whose
 // joint values are in (qv, qdv, qddv) and hands tau_j to `out(j, value)`.
@@ -17,70 +88,72 @@ __device__ __forceinline__ void rnea_eval(const T *mdl, const T (&qv)[N], const 
                                           const T (&qddv)[N], Out &&out) {
     T cs[N], sn[N];
     V3<T> fn[N], ff[N];  // per-link spatial force: moment n (rot), force f (lin)
-    V3<T> w, v, aw, av;  // link velocity / acceleration (rot, lin), link coordinates
-
-    {  // link 0: v_{-1} = 0, a_{-1} = (0, (0,0,+g)) -- multibody.rs:116-120
-        const Link<T> L = load_link(mdl, 0);
-        sin_cos<FAST>(qv[0], sn[0], cs[0]);
-        const M3<T> E = joint_rotation(L.Rp, cs[0], sn[0]);
-        const T g = T(kGravity);
-        const T qd0 = qdv[0];
-        w = v3(T(0), T(0), qd0);
-        v = v3(T(0), T(0), T(0));
-        aw = v3(T(0), T(0), qddv[0]);
-        av = v3(g * E.m[6], g * E.m[7], g * E.m[8]);  // E^T (0,0,g)
-        // I v with v = (w, 0):  n = I_o w,  f = -h x w
-        const V3<T> In = v3(L.Io.xz * qd0, L.Io.yz * qd0, L.Io.zz * qd0);
-        const V3<T> If = v3(-L.h.y * qd0, L.h.x * qd0, T(0));  // -h x (0,0,qd)
-        V3<T> An, Af;
-        inertia_mul(L, aw, av, An, Af);
-        ff[0] = cross_add(Af, w, If);
-        fn[0] = cross_add(An, w, In);
-    }
+    RneaState<T> st;
+    rnea_fwd0<T, FAST>(mdl, qv[0], qdv[0], qddv[0], st, sn[0], cs[0], fn[0], ff[0]);
 #pragma unroll
-    for (int j = 1; j < N; ++j) {
-        const Link<T> L = load_link(mdl, j);
-        sin_cos<FAST>(qv[j], sn[j], cs[j]);
-        const M3<T> E = joint_rotation(L.Rp, cs[j], sn[j]);
-        const T qdj = qdv[j];
-        // SpatialVelocity::transform (spatial.rs:110-116) on v and a
-        const V3<T> u = cross_sub(v, L.p, w);
-        const V3<T> ua = cross_sub(av, L.p, aw);
-        V3<T> wn = mul_t(E, w), vn = mul_t(E, u);
-        V3<T> awn = mul_t(E, aw), avn = mul_t(E, ua);
-        wn.z += qdj;        // multibody.rs:130
-        awn.z += qddv[j];   // multibody.rs:133
-        avn.x = fmadd(vn.y, qdj, avn.x);   // multibody.rs:135-138, v x (z qd) unrolled
-        avn.y = fmadd(-vn.x, qdj, avn.y);
-        awn.x = fmadd(wn.y, qdj, awn.x);
-        awn.y = fmadd(-wn.x, qdj, awn.y);
-        w = wn; v = vn; aw = awn; av = avn;
-        // f = I a + v x* (I v)   (multibody.rs:140)
-        V3<T> In, If, An, Af;
-        inertia_mul(L, w, v, In, If);
-        inertia_mul(L, aw, av, An, Af);
-        ff[j] = cross_add(Af, w, If);
-        fn[j] = cross_add(cross_add(An, w, In), v, If);
-    }
+    for (int j = 1; j < N; ++j) rnea_fwd<T, FAST>(mdl, j, qv[j], qdv[j], qddv[j], st, sn[j], cs[j], fn[j], ff[j]);
 
-    // Backward sweep: tau_i = n_i.z; f_{i-1} += X_i^-1 f_i  (multibody.rs:143-150)
+    // Backward sweep: tau_i = n_i.z (multibody.rs:144)
     reload_fence();
 #pragma unroll
     for (int j = N - 1; j >= 1; --j) {
         out(j, fn[j].z);
-        const T *c = mdl + j * kLinkStride;
-        const M3<T> Rp{{c[kE0 + 0], c[kE0 + 1], c[kE0 + 2], c[kE0 + 3], c[kE0 + 4], c[kE0 + 5],
-                        c[kE0 + 6], c[kE0 + 7], c[kE0 + 8]}};
-        const V3<T> p = v3(c[kP + 0], c[kP + 1], c[kP + 2]);
-        const T cj = cs[j], sj = sn[j];
-        // E x = R_p (Rz x)
-        const V3<T> zf = v3(fmadd(cj, ff[j].x, -sj * ff[j].y), fmadd(sj, ff[j].x, cj * ff[j].y), ff[j].z);
-        const V3<T> zn = v3(fmadd(cj, fn[j].x, -sj * fn[j].y), fmadd(sj, fn[j].x, cj * fn[j].y), fn[j].z);
-        const V3<T> fl = mul(Rp, zf);
-        ff[j - 1] = v3(ff[j - 1].x + fl.x, ff[j - 1].y + fl.y, ff[j - 1].z + fl.z);
-        fn[j - 1] = cross_add(mul_add(fn[j - 1], Rp, zn), p, fl);
+        rnea_bwd(mdl, j, cs[j], sn[j], ff[j], fn[j], ff[j - 1], fn[j - 1]);
     }
     out(0, fn[0].z);
+}
+
+// Segmented form for long chains: the per-link state the backward sweep needs (force 6,
+// cos/sin 2 -- 8 values per link, 240 VGPRs for 30 links, 2 waves/SIMD) is held for one
+// segment of ceil(N/S) links at a time.  Segments are processed top (leaf) first: each pass
+// reloads the inputs of links 0..hi-1 (`load(j, q, qd, qdd)`; L2/MALL-resident after the
+// first pass), recomputes the forward sweep up to its top link keeping only its own links'
+// state, and runs its part of the backward sweep; the force of its lowest link is carried
+// (with that link's cos/sin) into the next pass, where the same rnea_bwd step applies it --
+// so every tau is computed by exactly the operations of rnea_eval (bit-identical), at
+// (S+1)/2 times the forward-sweep work.
+template <typename T, int N, int S, bool FAST, typename Load, typename Out>
+__device__ __forceinline__ void rnea_eval_seg(const T *mdl, Load &&load, Out &&out) {
+    constexpr int L = (N + S - 1) / S;
+    T ccs = T(0), csn = T(0);
+    V3<T> cff = v3(T(0), T(0), T(0)), cfn = cff;
+    cfor_rev<S>([&](auto sc) {
+        constexpr int seg = decltype(sc)::value;
+        constexpr int lo = seg * L, hi = (lo + L < N) ? lo + L : N;
+        if constexpr (lo < N) {
+            T qv[hi], qdv[hi], qddv[hi];
+            cfor<0, hi>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                load(j, qv[j], qdv[j], qddv[j]);
+            });
+            T cs[hi - lo], sn[hi - lo];
+            V3<T> fn[hi - lo], ff[hi - lo];
+            RneaState<T> st;
+            cfor<0, hi>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                T s_, c_;
+                V3<T> fn_, ff_;
+                if constexpr (j == 0)
+                    rnea_fwd0<T, FAST>(mdl, qv[0], qdv[0], qddv[0], st, s_, c_, fn_, ff_);
+                else
+                    rnea_fwd<T, FAST>(mdl, j, qv[j], qdv[j], qddv[j], st, s_, c_, fn_, ff_);
+                if constexpr (j >= lo) {
+                    sn[j - lo] = s_; cs[j - lo] = c_; fn[j - lo] = fn_; ff[j - lo] = ff_;
+                }
+            });
+            reload_fence();
+            if constexpr (hi < N) rnea_bwd(mdl, hi, ccs, csn, cff, cfn, ff[hi - 1 - lo], fn[hi - 1 - lo]);
+            cfor_rev<hi - lo>([&](auto kc) {
+                constexpr int k = decltype(kc)::value, j = lo + k;
+                out(j, fn[k].z);
+                if constexpr (k > 0) {
+                    rnea_bwd(mdl, j, cs[k], sn[k], ff[k], fn[k], ff[k - 1], fn[k - 1]);
+                } else if constexpr (j > 0) {
+                    ccs = cs[0]; csn = sn[0]; cff = ff[0]; cfn = fn[0];
+                }
+            });
+        }
+    });
 }
 
 template <typename T, int N, bool FAST, typename Topo, typename Out>
@@ -113,6 +186,23 @@ __device__ __forceinline__ void rnea_lane(const T *mdl, const T *__restrict__ q,
     T qv[N], qdv[N], qddv[N];
     load_cfg<T, N>(q, qd, qdd, ld, off, qv, qdv, qddv);
     rnea_any<T, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
+}
+
+// Segmented lane (model-specialised kernels of long serial chains, tuning rnea_seg): S
+// segments, inputs reloaded per pass (rnea_eval_seg).
+template <typename T, int N, int S, bool FAST>
+__device__ __forceinline__ void rnea_lane_seg(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                              const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b,
+                                              int64_t ld) {
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    rnea_eval_seg<T, N, S, FAST>(
+        mdl,
+        [&](int j, T &x, T &y, T &z) {
+            x = ld_row(q, j * ld, off);
+            y = ld_row(qd, j * ld, off);
+            z = ld_row(qdd, j * ld, off);
+        },
+        [&](int j, T v) { st_row(tau, j * ld, off, v); });
 }
 
 // Paired lane (fp32 model-specialised kernels, spatial.hip.hpp f2): the configurations at

@@ -32,6 +32,7 @@ Tuning &tuning() {
         x.jit_variant = env_int("RB_JIT_VARIANT", x.jit_variant);
         x.pack = env_int("RB_PACK", x.pack);
         x.f64_tab = env_int("RB_F64_TAB", x.f64_tab);
+        x.rnea_seg = env_int("RB_RNEA_SEG", x.rnea_seg);
         return x;
     }();
     return t;

@@ -38,6 +38,9 @@ struct Tuning {
     // JIT fp64 kernels: 1 = table-assisted sincos (spatial.hip.hpp sincos_tab), 0 = the
     // pi/2-reduction minimax sincos_cw, -1 auto (on).
     int f64_tab = -1;
+    // JIT RNEA of serial chains: segments of the segmented form (rnea_eval_seg); 0/1 = the
+    // one-pass form, -1 auto (jit_rnea_seg in jit.cpp).
+    int rnea_seg = -1;
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
     int jit_variant = 0;
 };

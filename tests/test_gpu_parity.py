@@ -448,3 +448,40 @@ def test_paired_lane_kernels(kind, ffi, dev, fr3_text):
             assert (np.abs(res) / (1 + np.abs(xs[2]))).max() <= 1e-3, (pack, B, lay)
         if pack == 2:  # layouts agree bit for bit within one kernel form
             assert torch.equal(v, outs[(2, B, "soa" if lay == "tiled" else "tiled")][1])
+
+
+@pytest.mark.parametrize("seg", [2, 3, 5])
+def test_segmented_rnea_bit_identical(seg, ffi, dev, fr3_text):
+    """Segmented RNEA (tuning rnea_seg: the backward-sweep state held one segment at a time,
+    inputs reloaded per pass) runs exactly the one-pass operations: bit-identical outputs
+    for the 30- and 12-DOF chains and FR3, fp32 and fp64, SoA and tiled, ragged batches;
+    fp64 also against the oracle (1e-9)."""
+    from rigidbody_amd import chains
+
+    outs = {}
+    try:
+        for s in (0, seg):
+            ffi.set_tuning("rnea_seg", s)
+            for name, xml in (("chain30", chains.synthetic_chain_urdf(30)), ("chain12", chains.synthetic_chain_urdf(12)),
+                              ("fr3", fr3_text)):
+                mb = ffi.Multibody.from_urdf_string(xml)
+                n = mb.n
+                assert mb.kernel_path("rnea", False) == "jit"
+                for dt in (torch.float32, torch.float64):
+                    for B in (1, 300, 4096 + 5):
+                        rng = np.random.default_rng(B + n)
+                        x = [_t(rng.uniform(-2, 2, (n, B)), dev, dt) for _ in range(3)]
+                        outs[(s, name, dt, B, "soa")] = (xml, x, mb.rnea_batch(*x))
+                        xt = [ffi.to_tiled(a) for a in x]
+                        outs[(s, name, dt, B, "tiled")] = (xml, x, ffi.from_tiled(mb.rnea_batch_tiled(*xt, B), B))
+    finally:
+        ffi.set_tuning("rnea_seg", -1)
+    for (s, name, dt, B, lay), (xml, x, v) in outs.items():
+        if s == 0:
+            continue
+        ref = outs[(0, name, dt, B, lay)][2]
+        assert torch.equal(v, ref), (seg, name, dt, B, lay, (v - ref).abs().max().item())
+        if B == 300 and dt == torch.float64:  # fp32 one-pass accuracy: the golden tests
+            got = v.cpu().numpy()
+            want = _oracle(xml).rnea_batch(*[a.cpu().numpy() for a in x])
+            _close(got, want, 1e-9, f"seg={seg} {name}")

@@ -51,11 +51,19 @@ def main():
                 sets = bench.make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED, pad, lay)
                 launches[(lay, pad)] = bench.batch_launcher(mb, sets, a.kernel, dtype, lay, a.batch)
     lib = ffi.lib()
+    # every knob any variant sets is reset to the library default (tuning.hpp) before each
+    # variant, so a knob of one variant never leaks into the next
+    defaults = {"rnea_stream": -1, "grid_factor": 1, "jit": 1, "rnea_tile": 0, "rnea_nt": 3, "fd_nt": 3,
+                "jit_waves": -1, "opaque_consts": -1, "fd_stream": 0, "pack": -1, "f64_tab": -1, "rnea_seg": -1,
+                "jit_variant": 0}
+    used = {kv.split("=")[0] for v in a.variants for kv in v.split(",")} - {"streams"}
     keys = [(v, lp) for v in a.variants for lp in launches]
     res = {k: [] for k in keys}
     for r in range(a.rounds):
         for v, pad in keys:
             nstreams = 1
+            for k in used:
+                assert lib.rb_set_tuning(k.encode(), defaults[k]) == 0, ffi.last_error()
             for kv in v.split(","):
                 k, val = kv.split("=")
                 if k == "streams":
