@@ -195,14 +195,14 @@ hipError_t no_generic(const Multibody *mb) {
 constexpr uint32_t kPackMinBatch = 1u << 18;
 
 hipError_t jit_launch(const rbamd::JitKernel *jk, hipFunction_t fn, uint32_t B, void **args, hipStream_t s) {
-    const unsigned per_block = 256u * (unsigned)jk->pack;
+    const unsigned per_block = 256u * (unsigned)jk->pack * (unsigned)jk->tiles;
     const unsigned full = (unsigned)(((uint64_t)B + per_block - 1) / per_block);
     unsigned g = full;
     if (jk->stream) {
         const int f = rbamd::tuning().grid_factor < 1 ? 1 : rbamd::tuning().grid_factor;
         g = jk->resident * (unsigned)f < full ? jk->resident * (unsigned)f : full;
     }
-    return hipModuleLaunchKernel(fn, g, 1, 1, 256, 1, 1, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(fn, g, 1, 1, 256u * (unsigned)jk->tiles, 1, 1, 0, s, args, nullptr);
 }
 
 // tiled: the [ceil(B/256)][n][256] layout (kernels.hpp); the JIT lane kernels and the
@@ -776,6 +776,7 @@ int rb_set_tuning(const char *key, int value) {
     else if (k == "pack") t.pack = value;
     else if (k == "f64_tab") t.f64_tab = value;
     else if (k == "rnea_seg") t.rnea_seg = value;
+    else if (k == "rnea_tiles") t.rnea_tiles = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

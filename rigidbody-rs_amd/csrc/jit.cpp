@@ -75,6 +75,12 @@ int jit_pack(JitKind kind, bool f64, int n, bool stream) {
     return (kind == JitKind::Fd && n <= 8) ? 2 : 1;
 }
 
+int jit_tiles(JitKind kind, int pack, bool stream) {
+    if (kind != JitKind::Rnea || pack != 1 || stream) return 1;
+    const int v = tuning().rnea_tiles;
+    return v >= 4 ? 4 : (v >= 2 ? 2 : 1);
+}
+
 bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
 
 // Segments of the RNEA lane kernel (rnea_eval_seg) for a serial chain of n links; 1 = one pass.
@@ -89,7 +95,7 @@ int jit_rnea_seg(const Model &m, bool f64) {
 std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n, false)) +
-           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":s" + std::to_string(tuning().rnea_seg) + ":v" + std::to_string(tuning().jit_variant);
+           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":s" + std::to_string(tuning().rnea_seg) + ":b" + std::to_string(tuning().rnea_tiles) + ":v" + std::to_string(tuning().jit_variant);
 }
 
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack_req) {
@@ -151,7 +157,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         "  if (bA >= B) return;\n"
         "  const int64_t oA = (int64_t)(2u * blockIdx.x) * bs;\n"
         "  const int64_t oB = bA + 256u < B ? oA + bs : oA;\n";
-    std::string head_s = "extern \"C\" __global__ __launch_bounds__(256) ";
+    const int tiles = jit_tiles(kind, pack, stream);
+    std::string head_s = "extern \"C\" __global__ __launch_bounds__(" + std::to_string(256 * tiles) + ") ";
     if (const int w = jit_waves(kind, f64, m.n))
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
     head_s += "void ";
@@ -161,27 +168,35 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     if (kind == JitKind::Rnea) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
-        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
-        o << "  if (b >= B) return;\n";
         if (pack == 2) {
             o << pair_prologue;
             o << "  rbamd::dev::rnea_lane2<N, " << F
               << ", Topo>(kModel, q, qd, qdd, tau, oA, oB, threadIdx.x * 4u, ld);\n";
         } else if (stream) {  // SoA only (capi.cpp)
+            o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+            o << "  if (b >= B) return;\n";
             o << "  T qv[N], qdv[N], qddv[N];\n";
             o << "  rbamd::dev::load_cfg<T, N>(q, qd, qdd, ld, b * (uint32_t)sizeof(T), qv, qdv, qddv);\n";
             o << "  rbamd::dev::rnea_stream_lane<T, N, " << F
               << ", Topo>(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
         } else {
-            o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+            // tile k = blockIdx.x * tiles + threadIdx.x / 256 (wave-uniform: readfirstlane keeps
+            // the row bases in SGPRs, the saddr form), lane threadIdx.x % 256
+            if (tiles == 1)
+                o << "  const uint32_t tl = blockIdx.x, lane = threadIdx.x;\n";
+            else
+                o << "  const uint32_t tl = blockIdx.x * " << tiles
+                  << "u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), lane = threadIdx.x & 255u;\n";
+            o << "  if (tl * 256u + lane >= B) return;\n";
+            o << "  const int64_t o = (int64_t)tl * bs;\n";
             if (const int S = jit_rnea_seg(m, f64); S > 1)
                 o << "  rbamd::dev::rnea_lane_seg<T, N, " << S << ", " << F
-                  << ">(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
+                  << ">(kModel, q + o, qd + o, qdd + o, tau + o, lane, ld);\n";
             else
-                o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n";
+                o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, lane, ld);\n";
         }
         o << "}\n";
-        if (pack == 1 && jit_tile_ok(m.n, f64)) {  // SoA only
+        if (pack == 1 && tiles == 1 && jit_tile_ok(m.n, f64)) {  // SoA only
             o << head << "rb_jit_tile(const T *__restrict__ q, const T *__restrict__ qd, "
                  "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
             o << "  __shared__ T tile[3 * N * 256];\n";
@@ -272,6 +287,7 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stre
     JitKernel jk;
     jk.stream = stream;
     jk.pack = pack > 0 ? pack : jit_pack(kind, f64, m.n, stream);
+    jk.tiles = jit_tiles(kind, jk.pack, stream);
     int dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
@@ -286,7 +302,7 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stre
         jk.module = nullptr;
         return jk;
     }
-    if (kind == JitKind::Rnea && jk.pack == 1 && jit_tile_ok(m.n, f64) &&
+    if (kind == JitKind::Rnea && jk.pack == 1 && jk.tiles == 1 && jit_tile_ok(m.n, f64) &&
         hipModuleGetFunction(&jk.tile_function, jk.module, "rb_jit_tile") != hipSuccess)
         jk.tile_function = nullptr;
     e = hipModuleGetFunction(&jk.function, jk.module, "rb_jit_kernel");

@@ -33,6 +33,7 @@ struct JitKernel {
     hipFunction_t tile_function = nullptr;  // LDS-tiled, 16-byte global accesses (aligned SoA)
     bool stream = false;        // grid-stride form: launch a resident-sized grid
     int pack = 1;               // configurations per lane (2: paired fp32 lanes, 512 per block)
+    int tiles = 1;              // 256-configuration tiles per workgroup (256 x tiles threads)
     unsigned resident = 0;      // resident blocks (occupancy x CUs) for the stream form
     std::string error;          // non-empty when compilation failed
 };
@@ -53,6 +54,8 @@ bool jit_opaque(JitKind kind, bool f64, int n);
 int jit_waves(JitKind kind, bool f64, int n);
 // Configurations per lane of `kind`'s lane kernel (tuning `pack`): 2 = paired fp32 lanes.
 int jit_pack(JitKind kind, bool f64, int n, bool stream);
+// 256-configuration tiles per workgroup of `kind`'s lane kernel (tuning rnea_tiles).
+int jit_tiles(JitKind kind, int pack, bool stream);
 std::string jit_tag(JitKind kind, bool f64, int n);
 
 // hipRTC compilation only (no device needed): fills `code` with the code object.

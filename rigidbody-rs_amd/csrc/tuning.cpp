@@ -33,6 +33,7 @@ Tuning &tuning() {
         x.pack = env_int("RB_PACK", x.pack);
         x.f64_tab = env_int("RB_F64_TAB", x.f64_tab);
         x.rnea_seg = env_int("RB_RNEA_SEG", x.rnea_seg);
+        x.rnea_tiles = env_int("RB_RNEA_TILES", x.rnea_tiles);
         return x;
     }();
     return t;

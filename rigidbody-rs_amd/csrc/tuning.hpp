@@ -41,6 +41,9 @@ struct Tuning {
     // JIT RNEA of serial chains: segments of the segmented form (rnea_eval_seg); 0/1 = the
     // one-pass form, -1 auto (jit_rnea_seg in jit.cpp).
     int rnea_seg = -1;
+    // JIT RNEA lane kernel (one configuration per lane): 256-configuration tiles per
+    // workgroup (1, 2 or 4 -> 256 / 512 / 1024 threads).
+    int rnea_tiles = 1;
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
     int jit_variant = 0;
 };

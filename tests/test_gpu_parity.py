@@ -485,3 +485,27 @@ def test_segmented_rnea_bit_identical(seg, ffi, dev, fr3_text):
             got = v.cpu().numpy()
             want = _oracle(xml).rnea_batch(*[a.cpu().numpy() for a in x])
             _close(got, want, 1e-9, f"seg={seg} {name}")
+
+
+@pytest.mark.parametrize("tiles", [2, 4])
+def test_rnea_workgroup_tiles_bit_identical(tiles, ffi, dev, fr3_text):
+    """JIT RNEA with 2 / 4 tiles of 256 configurations per workgroup (tuning rnea_tiles)
+    gives the 1-tile kernel's outputs bit for bit: ragged batches (partial last workgroup,
+    partial last tile), SoA and tiled, fp32 and fp64."""
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    outs = {}
+    try:
+        for t in (1, tiles):
+            ffi.set_tuning("rnea_tiles", t)
+            for dt in (torch.float32, torch.float64):
+                for B in (1, 255, 257, 700, 1024, 4096 + 300):
+                    rng = np.random.default_rng(B)
+                    x = [_t(rng.uniform(-2, 2, (7, B)), dev, dt) for _ in range(3)]
+                    outs[(t, dt, B, "soa")] = mb.rnea_batch(*x)
+                    xt = [ffi.to_tiled(a) for a in x]
+                    outs[(t, dt, B, "tiled")] = ffi.from_tiled(mb.rnea_batch_tiled(*xt, B), B)
+    finally:
+        ffi.set_tuning("rnea_tiles", 1)
+    for (t, dt, B, lay), v in outs.items():
+        if t != 1:
+            assert torch.equal(v, outs[(1, dt, B, lay)]), (tiles, dt, B, lay)
