@@ -216,3 +216,31 @@ def test_jit_source_and_compile(ffi, fr3_text):
 def test_set_tuning_rejects_unknown_key(ffi):
     with pytest.raises(ffi.RigidBodyError, match="unknown tuning key"):
         ffi.set_tuning("no_such_knob", 1)
+
+
+def test_jit_kernel_forms_compile(ffi, fr3_text):
+    """Every model-specialised kernel form selectable by a tuning knob builds for gfx950
+    (hipRTC, no device) and its source carries the form: paired fp32 lanes (pack; FD default
+    for chains up to 8 links), table-assisted fp64 sincos (f64_tab, default on), segmented
+    RNEA (rnea_seg), multi-tile workgroups (rnea_tiles)."""
+    from rigidbody_amd import chains
+
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    c30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
+    assert "aba_lane2" in mb.jit_source(False, "fd")            # auto policy: paired FD
+    assert "aba_lane2" not in c30.jit_source(False, "fd")       # ... not for 30 links
+    assert "rnea_lane2" not in mb.jit_source(False, "rnea")     # RNEA one per lane
+    assert "sctab_init" in mb.jit_source(True, "rnea") and "sctab_init" not in mb.jit_source(False, "rnea")
+    forms = [("pack", 2, mb, "rnea", False, "rnea_lane2"), ("pack", 1, mb, "fd", False, "aba_lane<"),
+             ("f64_tab", 0, mb, "fd", True, "RB_SINCOS_TAB 0"), ("rnea_seg", 2, c30, "rnea", False, "rnea_lane_seg<T, N, 2"),
+             ("rnea_tiles", 4, mb, "rnea", True, "__launch_bounds__(1024)")]
+    defaults = {"pack": -1, "f64_tab": -1, "rnea_seg": -1, "rnea_tiles": 1}
+    try:
+        for key, val, m, kind, f64, marker in forms:
+            ffi.set_tuning(key, val)
+            assert marker in m.jit_source(f64, kind), (key, val)
+            assert m.jit_compile(f64=f64, kind=kind) > 1000, (key, val)
+            ffi.set_tuning(key, defaults[key])
+    finally:
+        for k, v in defaults.items():
+            ffi.set_tuning(k, v)
