@@ -91,7 +91,10 @@ __device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T
             const V3<T> nl = cross_add(mul(E, pa_n), L.p, fl);
             pAf = v3(pf[j - 1].x + fl.x, pf[j - 1].y + fl.y, pf[j - 1].z + fl.z);
             pAn = v3(pn[j - 1].x + nl.x, pn[j - 1].y + nl.y, pn[j - 1].z + nl.z);
-            IA = to_parent(E, L.p, Ia);
+            if constexpr (RB_SPLIT_ROT != 0)
+                IA = to_parent_split(L.Rp, cs[j], sn[j], E, L.p, Ia);
+            else
+                IA = to_parent(E, L.p, Ia);
             add_rigid(IA, load_link(mdl, j - 1));
         }
     }

@@ -93,6 +93,59 @@ __device__ __forceinline__ ArtI<T> to_parent(const M3<T> &E, const V3<T> &p, con
     return o;
 }
 
+// Model-specialised kernels (RB_SPLIT_ROT, set by jit.cpp): E = R_p Rz(q) with R_p a
+// compile-time constant, so E S E^T = R_p (Rz S Rz^T) R_p^T.  The Rz congruence of a
+// symmetric S uses the double angle (C = cos 2q, S2 = sin 2q):
+//   xx' = h + g C - xy S2,  yy' = h - g C + xy S2,  xy' = g S2 + xy C   (h, g = (xx +- yy)/2)
+//   xz' = c xz - s yz,      yz' = s xz + c yz,      zz' = zz
+// -- 10-14 FMAs where the folded E S E^T costs ~24 -- and the constant R_p congruence folds
+// to relabelling / sign changes for the signed-permutation frames URDF joints usually have.
+#ifndef RB_SPLIT_ROT
+#define RB_SPLIT_ROT 0
+#endif
+template <typename T>
+__device__ __forceinline__ S3<T> rot_sym_z(T c, T s, T C, T S2, const S3<T> &S) {
+    const T h = T(0.5) * (S.xx + S.yy), g = T(0.5) * (S.xx - S.yy);
+    return S3<T>{fmadd(g, C, fmadd(-S.xy, S2, h)), fmadd(g, S2, S.xy * C), fmadd(c, S.xz, -s * S.yz),
+                 fmadd(-g, C, fmadd(S.xy, S2, h)), fmadd(s, S.xz, c * S.yz), S.zz};
+}
+
+// to_parent with the symmetric blocks rotated as R_p (Rz S Rz^T) R_p^T.
+template <typename T>
+__device__ __forceinline__ ArtI<T> to_parent_split(const M3<T> &Rp, T c, T s, const M3<T> &E, const V3<T> &p,
+                                                   const ArtI<T> &I) {
+    const T C = fmadd(c, c, -s * s), S2 = (c + c) * s;
+    ArtI<T> J = I;
+    J.A = rot_sym(Rp, rot_sym_z(c, s, C, S2, I.A));
+    J.M = rot_sym(Rp, rot_sym_z(c, s, C, S2, I.M));
+    // B and the shift as to_parent, with the rotated symmetric blocks passed through unchanged
+    const M3<T> B1 = rot_full(E, I.B);
+    const S3<T> M1 = J.M;
+    const T m[9] = {M1.xx, M1.xy, M1.xz, M1.xy, M1.yy, M1.yz, M1.xz, M1.yz, M1.zz};
+    M3<T> B2;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        B2.m[0 + k] = fmadd(-p.z, m[3 + k], fmadd(p.y, m[6 + k], B1.m[0 + k]));
+        B2.m[3 + k] = fmadd(p.z, m[0 + k], fmadd(-p.x, m[6 + k], B1.m[3 + k]));
+        B2.m[6 + k] = fmadd(-p.y, m[0 + k], fmadd(p.x, m[3 + k], B1.m[6 + k]));
+    }
+    const T P[9] = {T(0), -p.z, p.y, p.z, T(0), -p.x, -p.y, p.x, T(0)};
+    auto a = [&](int r, int cc, T base) {
+        T acc = base;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc = fmadd(P[3 * r + k], B1.m[3 * cc + k], acc);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc = fmadd(B2.m[3 * r + k], P[3 * cc + k], acc);
+        return acc;
+    };
+    const S3<T> A1 = J.A;
+    ArtI<T> o;
+    o.A = S3<T>{a(0, 0, A1.xx), a(0, 1, A1.xy), a(0, 2, A1.xz), a(1, 1, A1.yy), a(1, 2, A1.yz), a(2, 2, A1.zz)};
+    o.B = B2;
+    o.M = M1;
+    return o;
+}
+
 template <typename T>
 __device__ __forceinline__ void add_rigid(ArtI<T> &I, const Link<T> &L) {
     I.A.xx += L.Io.xx; I.A.xy += L.Io.xy; I.A.xz += L.Io.xz;

@@ -777,6 +777,7 @@ int rb_set_tuning(const char *key, int value) {
     else if (k == "f64_tab") t.f64_tab = value;
     else if (k == "rnea_seg") t.rnea_seg = value;
     else if (k == "rnea_tiles") t.rnea_tiles = value;
+    else if (k == "split_rot") t.split_rot = value;
     else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
     return RB_OK;
 }

@@ -36,7 +36,10 @@ __device__ __forceinline__ void crba_eval(const T *mdl, const T (&qv)[N], Out &&
         if (i > 0) {
             const Link<T> L = load_link(mdl, i);
             const M3<T> E = joint_rotation(L.Rp, cs[i], sn[i]);
-            Ic = to_parent(E, L.p, Ic);
+            if constexpr (RB_SPLIT_ROT != 0)
+                Ic = to_parent_split(L.Rp, cs[i], sn[i], E, L.p, Ic);
+            else
+                Ic = to_parent(E, L.p, Ic);
             add_rigid(Ic, load_link(mdl, i - 1));
         }
     }

@@ -95,7 +95,7 @@ int jit_rnea_seg(const Model &m, bool f64) {
 std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n, false)) +
-           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":s" + std::to_string(tuning().rnea_seg) + ":b" + std::to_string(tuning().rnea_tiles) + ":v" + std::to_string(tuning().jit_variant);
+           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":s" + std::to_string(tuning().rnea_seg) + ":b" + std::to_string(tuning().rnea_tiles) + ":r" + std::to_string(tuning().split_rot) + ":v" + std::to_string(tuning().jit_variant);
 }
 
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack_req) {
@@ -113,6 +113,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
     const bool tab = jit_f64_tab(f64);
     o << "#define RB_SINCOS_TAB " << (tab ? 1 : 0) << "\n";
+    o << "#define RB_SPLIT_ROT " << (tuning().split_rot != 0 ? 1 : 0) << "\n";
     o << (kind == JitKind::Rnea                               ? "#include \"rnea_body.hip.hpp\"\n"
           : (kind == JitKind::Fd || kind == JitKind::Rollout) ? "#include \"aba_body.hip.hpp\"\n"
           : kind == JitKind::Crba                             ? "#include \"crba_body.hip.hpp\"\n"

@@ -34,6 +34,7 @@ Tuning &tuning() {
         x.f64_tab = env_int("RB_F64_TAB", x.f64_tab);
         x.rnea_seg = env_int("RB_RNEA_SEG", x.rnea_seg);
         x.rnea_tiles = env_int("RB_RNEA_TILES", x.rnea_tiles);
+        x.split_rot = env_int("RB_SPLIT_ROT", x.split_rot);
         return x;
     }();
     return t;

@@ -44,6 +44,9 @@ struct Tuning {
     // JIT RNEA lane kernel (one configuration per lane): 256-configuration tiles per
     // workgroup (1, 2 or 4 -> 256 / 512 / 1024 threads).
     int rnea_tiles = 1;
+    // JIT ABA / CRBA: rotate symmetric inertia blocks as R_p (Rz S Rz^T) R_p^T with the double
+    // angle (artinertia.hip.hpp to_parent_split); 0 = the folded E S E^T.
+    int split_rot = 1;
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
     int jit_variant = 0;
 };
