@@ -113,7 +113,22 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
     const bool tab = jit_f64_tab(f64);
     o << "#define RB_SINCOS_TAB " << (tab ? 1 : 0) << "\n";
-    o << "#define RB_SPLIT_ROT " << (tuning().split_rot != 0 ? 1 : 0) << "\n";
+    // Split joint rotation (artinertia.hip.hpp to_parent_split): pays only when every R_p is a
+    // signed permutation (its congruence then folds away); a dense constant R_p (general-axis
+    // frames, trees) makes it costlier than the folded E S E^T.
+    bool perm = true;
+    for (int i = 0; i < m.n && perm; ++i)
+        for (int r = 0; r < 3; ++r) {
+            int ones = 0;
+            for (int c = 0; c < 3; ++c) {
+                const double v = pk[(size_t)i * kLinkStride + kE0 + 3 * r + c];
+                if (v == 1.0 || v == -1.0) ++ones;
+                else if (v != 0.0) perm = false;
+            }
+            if (ones != 1) perm = false;
+        }
+    const int sr = tuning().split_rot;
+    o << "#define RB_SPLIT_ROT " << ((sr > 0 || (sr < 0 && perm)) ? 1 : 0) << "\n";
     o << (kind == JitKind::Rnea                               ? "#include \"rnea_body.hip.hpp\"\n"
           : (kind == JitKind::Fd || kind == JitKind::Rollout) ? "#include \"aba_body.hip.hpp\"\n"
           : kind == JitKind::Crba                             ? "#include \"crba_body.hip.hpp\"\n"

@@ -45,8 +45,9 @@ struct Tuning {
     // workgroup (1, 2 or 4 -> 256 / 512 / 1024 threads).
     int rnea_tiles = 1;
     // JIT ABA / CRBA: rotate symmetric inertia blocks as R_p (Rz S Rz^T) R_p^T with the double
-    // angle (artinertia.hip.hpp to_parent_split); 0 = the folded E S E^T.
-    int split_rot = 1;
+    // angle (artinertia.hip.hpp to_parent_split); 0 = the folded E S E^T; -1 auto = on when
+    // every joint frame R_p is a signed permutation.
+    int split_rot = -1;
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
     int jit_variant = 0;
 };

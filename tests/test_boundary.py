@@ -233,8 +233,10 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "sctab_init" in mb.jit_source(True, "rnea") and "sctab_init" not in mb.jit_source(False, "rnea")
     forms = [("pack", 2, mb, "rnea", False, "rnea_lane2"), ("pack", 1, mb, "fd", False, "aba_lane<"),
              ("f64_tab", 0, mb, "fd", True, "RB_SINCOS_TAB 0"), ("rnea_seg", 2, c30, "rnea", False, "rnea_lane_seg<T, N, 2"),
-             ("rnea_tiles", 4, mb, "rnea", True, "__launch_bounds__(1024)")]
-    defaults = {"pack": -1, "f64_tab": -1, "rnea_seg": -1, "rnea_tiles": 1}
+             ("rnea_tiles", 4, mb, "rnea", True, "__launch_bounds__(1024)"),
+             ("split_rot", 0, mb, "crba", False, "RB_SPLIT_ROT 0")]
+    defaults = {"pack": -1, "f64_tab": -1, "rnea_seg": -1, "rnea_tiles": 1, "split_rot": -1}
+    assert "RB_SPLIT_ROT 1" in mb.jit_source(False, "fd")  # FR3 frames are signed permutations
     try:
         for key, val, m, kind, f64, marker in forms:
             ffi.set_tuning(key, val)
