@@ -36,8 +36,10 @@ DT = {"f32": torch.float32, "f64": torch.float64}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000, help="timed steps (~21 ms at the headline: long enough "
-                                                                 "to average out clock transients)")
+    ap.add_argument("--steps", type=int, default=4000,
+                    help="timed steps (~90 ms at the headline): long enough to average over the clock / "
+                         "power phases a sustained load goes through (a 1000-step window lands either in a "
+                         "~20.3 or a ~25 us phase on some boxes; tools/drift.py, DESIGN.md §8)")
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--batch", type=int, default=1 << 20, help="configurations per GPU per step")
     ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
@@ -55,6 +57,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the timed batches rotate over (1 = strictly serial launches, the "
                          "headline; the overlapped 2-stream rate is reported under 'secondary')")
+    ap.add_argument("--sync-every", type=int, default=0,
+                    help="host-synchronize every N timed steps (0 = never; the sync time stays inside the "
+                         "timed region)")
     ap.add_argument("--spinup-ms", type=float, default=300.0,
                     help="untimed launches before the warmup so the GPU clock reaches steady state")
     return ap.parse_args()
@@ -138,7 +143,7 @@ def set_bytes(n, B, esize, kernel):
     return (8 if kernel == "rnea_fd" else 4) * n * B * esize
 
 
-def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1):
+def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1, sync_every=0):
     """launch(i, stream_ptr) issues step i.  Warmup, then exactly `steps` launches
     bracketed by barrier + synchronize and one hipEvent pair on the launch stream (no
     per-launch events inside the timed region: an event record between launches on one
@@ -169,6 +174,8 @@ def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1):
         st.wait_event(e0)
     for i in range(steps):
         launch(i, sps[i % streams])
+        if sync_every and (i + 1) % sync_every == 0 and i + 1 < steps:
+            torch.cuda.synchronize()  # host waits for the queue to drain (inside the timed region)
     for st, end in zip(strs[1:], ends[1:]):
         end.record(st)
         main.wait_event(end)
@@ -252,8 +259,10 @@ def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED):
     return launch
 
 
-def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1, layout="soa", B=None):
-    return time_launches(batch_launcher(mb, sets, kernel, dtype, layout, B), steps, warmup, world, spinup_ms, streams)
+def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1, layout="soa", B=None,
+              sync_every=0):
+    return time_launches(batch_launcher(mb, sets, kernel, dtype, layout, B), steps, warmup, world, spinup_ms, streams,
+                         sync_every)
 
 
 def side_workloads(mb7, a, rotate_gib):
@@ -357,7 +366,7 @@ def main():
     nsets = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / per_set)))
     sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, rdist.rank_seed(chains.SEED, rank), layout=a.layout)
     wall, kern_avg_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms, a.streams,
-                                  a.layout, a.batch)
+                                  a.layout, a.batch, a.sync_every)
     wall, kern_avg_ms = rdist.max_over_ranks([wall, kern_avg_ms], world, torch.device("cuda"))
     evals = world * a.batch * a.steps
     value = evals / wall

@@ -1,12 +1,13 @@
 #!/bin/bash
 # GPU-box recipe for the round's committed profiles: the default bench line, a kernel
-# trace (--kernel-trace --stats) of the headline command, and four separate PMC passes.
+# trace (--kernel-trace --stats) of the headline command (its own printed bench line is
+# checked against its trace by tools/trace_check.py), and four separate PMC passes.
 # Each step is time-limited; the chain stops at the first failure.
 # usage (via gpurun): tools/profile_round.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$PWD
 O=$R/gpurun_out
-HEAD="python3 $R/bench.py --no-cpu-baseline --no-secondary --steps 100 --warmup 10"
+HEAD="python3 $R/bench.py --no-cpu-baseline --no-secondary"
 export TMPDIR=/tmp
 tools/gpu_steps.sh \
   bench 400 "python bench.py" \
