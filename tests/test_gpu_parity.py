@@ -509,3 +509,36 @@ def test_rnea_workgroup_tiles_bit_identical(tiles, ffi, dev, fr3_text):
     for (t, dt, B, lay), v in outs.items():
         if t != 1:
             assert torch.equal(v, outs[(1, dt, B, lay)]), (tiles, dt, B, lay)
+
+
+@pytest.mark.parametrize("knob", ["fd_stream", "rnea_stream"])
+def test_resident_grid_stride_forms(knob, ffi, dev, fr3_text):
+    """The resident grid-stride JIT forms (A/B knobs fd_stream / rnea_stream: a resident-sized
+    grid walking the batch with a register prefetch of the next block) meet the oracle
+    tolerances on ragged batches that take several passes per block: fp64 1e-9 (rnea tau; fd
+    through the torque residual 1e-8), fp32 1e-4 (rnea) / residual 1e-3 (fd); SoA, and tiled
+    for fd (the tiled RNEA launch uses the lane kernel)."""
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    om = _oracle(fr3_text)
+    kind = "fd" if knob == "fd_stream" else "rnea"
+    try:
+        ffi.set_tuning(knob, 1)
+        for dt, tol in ((torch.float64, 1e-9), (torch.float32, 1e-4)):
+            for B in (1, 257, 3 * 65536 + 5, (1 << 20) + 77):
+                rng = np.random.default_rng(B)
+                x = [_t(rng.uniform(-2, 2, (7, B)), dev, dt) for _ in range(3)]
+                outs = {"soa": (mb.rnea_batch if kind == "rnea" else mb.fd_batch)(*x)}
+                if kind == "fd":
+                    outs["tiled"] = ffi.from_tiled(mb.fd_batch_tiled(*[ffi.to_tiled(a) for a in x], B), B)
+                cols = np.unique(np.r_[np.arange(min(B, 300)), np.arange(max(0, B - 300), B)])
+                xs = [a.double().cpu().numpy()[:, cols] for a in x]
+                for lay, v in outs.items():
+                    got = v.double().cpu().numpy()[:, cols]
+                    if kind == "rnea":
+                        _close(got, om.rnea_batch(*xs), tol, f"{knob} {dt} B={B} {lay}")
+                    else:
+                        res = om.rnea_batch(xs[0], xs[1], got) - xs[2]
+                        lim = 1e-8 if dt == torch.float64 else 1e-3
+                        assert (np.abs(res) / (1 + np.abs(xs[2]))).max() <= lim, (knob, dt, B, lay)
+    finally:
+        ffi.set_tuning(knob, 0 if knob == "fd_stream" else -1)
