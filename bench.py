@@ -187,6 +187,44 @@ def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1, sync_e
     return t1 - t0, e0.elapsed_time(e1) / steps
 
 
+def time_graph(launch, steps, per_graph=100, spinup_ms=100.0):
+    """The same launches replayed from a HIP graph: `per_graph` consecutive launches (rotating
+    input sets) are stream-captured once (torch.cuda.graph), then the graph is replayed
+    steps / per_graph times between one hipEvent pair -- the host issues one graph launch per
+    `per_graph` steps instead of one C-ABI call per step, which is what a short kernel (a
+    65536-configuration batch runs ~4 us) needs.  Returns (wall s, device ms per step)."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # JIT compile + warm outside the capture
+        sp = ctypes.c_void_p(side.cuda_stream)
+        for i in range(per_graph):
+            launch(i, sp)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for i in range(per_graph):
+            launch(i, sp)
+    torch.cuda.synchronize()
+    t_spin = time.perf_counter()
+    while (time.perf_counter() - t_spin) * 1e3 < spinup_ms:
+        g.replay()
+        torch.cuda.synchronize()
+    reps = max(1, steps // per_graph)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    del g
+    return t1 - t0, e0.elapsed_time(e1) / (reps * per_graph)
+
+
 def batch_launcher(mb, sets, kernel, dtype, layout="soa", B=None):
     """Closure issuing the batched entry point(s) of `kernel` on input set i % len(sets)."""
     lib = ffi.lib()
@@ -270,7 +308,7 @@ def side_workloads(mb7, a, rotate_gib):
     sec = {}
     steps = max(20, a.steps // 4)
 
-    def one(name, mb, kernel, dt_name, B=a.batch):
+    def one(name, mb, kernel, dt_name, B=a.batch, graph=False):
         ds = DT[dt_name]
         es = 4 if dt_name == "f32" else 8
         per = set_bytes(mb.n, B, es, kernel)
@@ -280,15 +318,20 @@ def side_workloads(mb7, a, rotate_gib):
         sec[name] = {"evals_per_s": B * steps / w, "kernel_ms_avg": km, "batch": B, "layout": a.layout,
                      "hbm_frac": per / (km * 1e-3) / HBM_PEAK,
                      "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64") for k in kernel.split("_"))}
+        if graph:  # the same launches replayed from a HIP graph
+            gw, gkm = time_graph(batch_launcher(mb, sets, kernel, ds, a.layout, B), steps)
+            sec[name + "_graph"] = {"evals_per_s": B * steps / gw, "kernel_ms_avg": gkm, "batch": B,
+                                    "layout": a.layout, "hbm_frac": per / (gkm * 1e-3) / HBM_PEAK,
+                                    "launch": "HIP graph of 100 captured C-ABI launches, replayed"}
         del sets
         torch.cuda.empty_cache()
 
-    one("rnea_fr3_f32_b65536", mb7, "rnea", "f32", 65536)    # config 2
-    one("fd_fr3_f32_b65536", mb7, "fd", "f32", 65536)        # config 3
+    one("rnea_fr3_f32_b65536", mb7, "rnea", "f32", 65536, graph=True)    # config 2
+    one("fd_fr3_f32_b65536", mb7, "fd", "f32", 65536, graph=True)        # config 3
     one("rnea_fr3_f64", mb7, "rnea", "f64")
     one("fd_fr3_f32", mb7, "fd", "f32")
     one("fd_fr3_f64", mb7, "fd", "f64")
-    one("rnea_fd_fr3_f64_b131072", mb7, "rnea_fd", "f64", 1 << 17)  # config 4, one GPU's 2^17 shard
+    one("rnea_fd_fr3_f64_b131072", mb7, "rnea_fd", "f64", 1 << 17, graph=True)  # config 4, one GPU's 2^17 shard
     mb30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     mb30.upload()
     one("rnea_chain30_f32", mb30, "rnea", "f32")             # config 5
