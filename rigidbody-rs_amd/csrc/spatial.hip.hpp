@@ -36,10 +36,10 @@ __device__ __forceinline__ double fmadd(double a, double b, double c) { return _
 // Paired fp32 lanes (model-specialised fp32 kernels, tuning `pack`): a lane evaluates two
 // configurations at once as a 2-wide vector, so every FMA/MUL/ADD of the recursion becomes
 // one v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (FR3 RNEA: 646 VALU instructions per PAIR
-// vs 586 per configuration).  gfx950 already issues a wave64 v_fma_f32 in 2 cycles, so this
-// is not a throughput doubling; what pays is the second independent dependency chain per
-// lane for the latency-bound forward dynamics (FR3: 28.7 vs 30.7 us).  Only
-// sin/cos and 1/x stay per element; both halves run identical instruction sequences.
+// vs 586 per configuration).  It pays for the issue-/latency-bound forward dynamics (FR3:
+// 28.0 vs 29.0-30.7 us; the same pairing as two scalar FMAs per operation: 33.7 us, DESIGN.md
+// §4), not for the memory-bound RNEA.  Only sin/cos and 1/x stay per element; both halves run
+// identical instruction sequences.
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fmadd(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
