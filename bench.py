@@ -2,11 +2,17 @@
 """Benchmark: batched RNEA (fr3 7-DOF) evals/s on MI355X, BASELINE.json's metric.
 
 One step = one launch of the RNEA kernel over one batch of B configurations
-(default B = 2^20 per GPU, fp32, SoA, inputs already resident in HBM).  The input
-sets rotate through >1 GiB of device memory so the 256 MiB Infinity Cache cannot
-serve them.  N > 1: one process per GPU (torch.distributed.run), the model is loaded
-on rank 0 and broadcast as a blob over RCCL, every rank evaluates its own batch
-(weak scaling, no data-path collective), timing is max over ranks.
+(default B = 2^20 per GPU, fp64 -- the reference's `Real = f64`, lib.rs:15 -- tiled
+[B/256][n][256] layout, inputs already resident in HBM).  The input sets rotate through
+>1 GiB of device memory so the 256 MiB Infinity Cache cannot serve them.
+
+Multi-GPU: one process per GPU.  `--gpus N` with N > 1 started by hand spawns N fresh
+child ranks itself (this parent never touches the GPU and relays rank 0's JSON line);
+under torch.distributed.run the ranks come from the environment.  The model is loaded on
+rank 0 and broadcast as a blob over RCCL; each rank evaluates its own 2^20 batch
+(`--split weak`, the default) or its contiguous shard of one global 2^20 batch
+(`--split strong`, SURVEY §8(e): 2^17 per GPU at N = 8).  No collective touches the data
+path; timing is max over ranks.  A weak run also reports the strong split beside it.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §5 for how roofline/cpu_baseline are
 derived; profiles/ holds the rocprofv3 summaries these numbers are checked against.
@@ -15,34 +21,31 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-
 REPO = os.path.dirname(os.path.abspath(__file__))
-for _p in (REPO, os.path.join(REPO, "rigidbody-rs_amd")):
-    if _p not in sys.path:
-        sys.path.insert(0, _p)
-
-from rigidbody_amd import chains, ffi  # noqa: E402
-from rigidbody_amd import dist as rdist  # noqa: E402
-
+METRIC = "RNEA evals/sec (fr3 7-DOF, batch 2^20) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (/opt/skills/guides/MI355X_MICROARCH.md)
-DT = {"f32": torch.float32, "f64": torch.float64}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); N > 1 without WORLD_SIZE in the environment spawns N ranks")
     ap.add_argument("--steps", type=int, default=4000,
-                    help="timed steps (~90 ms at the headline): long enough to average over the clock / "
-                         "power phases a sustained load goes through (a 1000-step window lands either in a "
-                         "~20.3 or a ~25 us phase on some boxes; tools/drift.py, DESIGN.md §8)")
+                    help="timed steps: long enough to average over the clock / power phases a sustained "
+                         "load goes through (tools/drift.py, DESIGN.md §5)")
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="configurations per GPU per step")
-    ap.add_argument("--dtype", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--batch", type=int, default=1 << 20,
+                    help="configurations per GPU per step (--split weak) or in total (--split strong)")
+    ap.add_argument("--split", choices=["weak", "strong"], default="weak",
+                    help="weak: every rank evaluates its own --batch; strong: the ranks shard one --batch")
+    ap.add_argument("--dtype", choices=["f32", "f64"], default="f64",
+                    help="f64 = the reference's Real (lib.rs:15), the headline; f32 is a reduced-precision "
+                         "variant reported under 'secondary'")
     ap.add_argument("--kernel", choices=["rnea", "fd", "rnea_fd"], default="rnea",
                     help="rnea_fd = SURVEY §8(d) config 4: each step runs RNEA then forward dynamics on "
                          "its torques (q, qd, qdd -> tau -> qdd'), 8·N·s bytes per configuration")
@@ -53,75 +56,141 @@ def parse():
     ap.add_argument("--rotate-gib", type=float, default=1.25, help="device memory the input sets span")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU work budget of the baseline sample")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the fp64 / forward-dynamics side lines")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the side lines")
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the timed batches rotate over (1 = strictly serial launches, the "
                          "headline; the overlapped 2-stream rate is reported under 'secondary')")
     ap.add_argument("--sync-every", type=int, default=0,
-                    help="host-synchronize every N timed steps (0 = never; the sync time stays inside the "
-                         "timed region)")
+                    help="host-synchronize every N timed steps (0 = never; inside the timed region)")
     ap.add_argument("--spinup-ms", type=float, default=300.0,
                     help="untimed launches before the warmup so the GPU clock reaches steady state")
-    return ap.parse_args()
+    ap.add_argument("--stub", action="store_true",
+                    help="CPU rehearsal of the launch / rank / reporting plumbing (gloo, no kernels, "
+                         "no GPU); the JSON line says data='stub'")
+    return ap.parse_args(argv)
 
 
-def init_dist():
-    """One process per GPU (torch.distributed.run).  Backend "nccl" = RCCL over xGMI;
-    RB_DIST_BACKEND=gloo rehearses the multi-process path with several ranks sharing
-    one GPU (ranks map to devices round-robin)."""
+# ------------------------------------------------------------------ rank spawning
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(a, argv):
+    """Parent of an N-rank run started as `python bench.py --gpus N`: starts N fresh child
+    processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, the same
+    arguments), waits for all, relays rank 0's stdout and returns non-zero if any rank
+    failed.  Never imports torch, never touches a GPU."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    base = dict(os.environ, MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port,
+                WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus))
+    import tempfile
+
+    procs = []
+    with tempfile.TemporaryFile() as out0:
+        for r in range(a.gpus):
+            env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                          stdout=out0 if r == 0 else subprocess.DEVNULL))
+        # a rank that fails leaves the others blocked in a collective: stop them (exact PIDs)
+        failed = None
+        while any(p.poll() is None for p in procs):
+            for r, p in enumerate(procs):
+                if p.returncode not in (None, 0) and failed is None:
+                    failed = r
+                    for q in procs:
+                        if q.poll() is None:
+                            q.terminate()
+            time.sleep(0.1)
+        for p in procs:
+            p.wait()
+        out0.seek(0)
+        # rank 0's JSON line to stdout; anything else it printed (library chatter) to stderr
+        for ln in out0.read().decode(errors="replace").splitlines():
+            (sys.stdout if ln.startswith("{") else sys.stderr).write(ln + "\n")
+        sys.stdout.flush()
+    bad = [(r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0]
+    if bad:
+        print(f"bench.py: rank(s) failed (rank, exit status): {bad}", file=sys.stderr)
+        first = dict(bad).get(failed, bad[0][1]) if failed is not None else bad[0][1]
+        return first if 0 < first < 256 else 1
+    return 0
+
+
+if __name__ == "__main__":
+    _ARGS = parse()
+    if _ARGS.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(_ARGS, sys.argv[1:]))
+
+# ----------------------------------------------------------------- rank process
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+for _p in (REPO, os.path.join(REPO, "rigidbody-rs_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from rigidbody_amd import chains, ffi  # noqa: E402
+from rigidbody_amd import dist as rdist  # noqa: E402
+
+DT = {"f32": torch.float32, "f64": torch.float64}
+
+
+def init_dist(a):
+    """One process per GPU.  Backend "nccl" = RCCL over xGMI; RB_DIST_BACKEND=gloo rehearses
+    the multi-process path (ranks then share GPUs round-robin); --stub uses gloo on CPU.
+    Returns (world, rank, device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local % ndev)
+    if a.stub:
+        dev = torch.device("cpu")
+    else:
+        ndev = max(1, torch.cuda.device_count())
+        dev = torch.device("cuda", local % ndev)
+        torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        backend = os.environ.get("RB_DIST_BACKEND", "nccl")
+        backend = "gloo" if a.stub else os.environ.get("RB_DIST_BACKEND", "nccl")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local % ndev))
+            dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    return world, rank, local
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
+        world = dist.get_world_size()
+    if a.gpus > 1 or world > 1:
+        assert world == a.gpus, f"--gpus {a.gpus} but the job has {world} rank(s)"
+    return world, rank, dev
 
 
-def load_model(world, rank, dof):
+def load_model(world, rank, dof, dev):
     """Rank 0 parses the URDF; the packed fp64 model blob is broadcast over RCCL
     (rigidbody_amd.dist.broadcast_model)."""
     def make():
         return ffi.Multibody.new() if dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(dof))
 
-    mb = rdist.broadcast_model(make, rank, world, torch.device("cuda"))
-    mb.upload()
+    mb = rdist.broadcast_model(make, rank, world, dev)
+    if dev.type == "cuda":
+        mb.upload()
     return mb
 
 
-def make_sets(mb, B, dtype, kernel, nsets, seed, pad=0, layout="soa"):
+def make_sets(mb, B, dtype, kernel, nsets, seed, layout="soa"):
     """nsets independent (inputs, outputs) sets on the device.  rnea / rnea_fd read
     (q, qd, qdd); fd reads (q, qd, tau).  rnea_fd has two outputs (tau, qdd').
-    pad > 0: rows are ld = B + pad elements apart ([n, ld] buffers used as [n, B] views).
     layout "tiled": [ceil(B/256), n, 256] tensors (rigidbody_batch.h), filled with the
     same values as the SoA sets (device fill, then rb_to_tiled)."""
     if layout == "tiled":
-        # pad > 0 (tiled): array k of a set starts k * pad elements into its own buffer --
-        # staggers the arrays' base addresses (channel-aliasing experiments, tools/ab_bench.py)
-        def placed(t, k):
-            tt = ffi.to_tiled(t)
-            if not pad:
-                return tt
-            buf = torch.empty(k * pad + tt.numel(), dtype=tt.dtype, device=tt.device)
-            v = buf[k * pad:].view(tt.shape)
-            v.copy_(tt)
-            return v
-
         sets = []
         for ins, outs in make_sets(mb, B, dtype, kernel, nsets, seed):
-            sets.append(([placed(t, k) for k, t in enumerate(ins)],
-                         [placed(t, len(ins) + k) for k, t in enumerate(outs)]))
+            sets.append(([ffi.to_tiled(t) for t in ins], [ffi.to_tiled(t) for t in outs]))
             del ins, outs
         torch.cuda.synchronize()
         return sets
-    ld = B + pad
     lim = mb.limits()
     kinds = ("q", "qd", "tau") if kernel == "fd" else ("q", "qd", "qdd")
     nout = 2 if kernel == "rnea_fd" else 1
@@ -130,17 +199,28 @@ def make_sets(mb, B, dtype, kernel, nsets, seed, pad=0, layout="soa"):
         ins = []
         for k, kind in enumerate(kinds):
             lo, hi = chains.input_ranges(lim, kind)
-            t = torch.empty((mb.n, ld), dtype=dtype, device="cuda")[:, :B]
+            t = torch.empty((mb.n, B), dtype=dtype, device="cuda")
             ffi.fill_uniform(t, lo, hi, seed + 1000 * s + k)
             ins.append(t)
-        outs = [torch.empty((mb.n, ld), dtype=dtype, device="cuda")[:, :B] for _ in range(nout)]
+        outs = [torch.empty((mb.n, B), dtype=dtype, device="cuda") for _ in range(nout)]
         sets.append((ins, outs))
     torch.cuda.synchronize()
     return sets
 
 
 def set_bytes(n, B, esize, kernel):
+    """Algorithmic HBM bytes: q, qd, qdd|tau read + tau|qdd written, 4·N·s per
+    configuration; rnea_fd counts both kernels."""
     return (8 if kernel == "rnea_fd" else 4) * n * B * esize
+
+
+def nsets_for(n, B, esize, kernel, rotate_gib):
+    return max(2, int(np.ceil(rotate_gib * (1 << 30) / max(1, set_bytes(n, B, esize, kernel)))))
+
+
+def barrier(world):
+    if world > 1:
+        torch.distributed.barrier()
 
 
 def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1, sync_every=0):
@@ -148,8 +228,8 @@ def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1, sync_e
     bracketed by barrier + synchronize and one hipEvent pair on the launch stream (no
     per-launch events inside the timed region: an event record between launches on one
     stream inflates a ~22 us step to ~32 us).  With streams > 1 consecutive steps rotate
-    over that many streams (independent batches overlap the previous launch's ramp and
-    tail); the event pair then spans all of them.  Returns (wall s, device ms per step)."""
+    over that many streams; the event pair then spans all of them.
+    Returns (wall s, device ms per step)."""
     main = torch.cuda.current_stream()
     strs = [main] + [torch.cuda.Stream() for _ in range(streams - 1)]
     sps = [ctypes.c_void_p(st.cuda_stream) for st in strs]
@@ -165,9 +245,8 @@ def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1, sync_e
         launch(i, sps[i % streams])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ends = [torch.cuda.Event() for _ in strs]
-    if world > 1:
-        torch.distributed.barrier()
     torch.cuda.synchronize()
+    barrier(world)
     t0 = time.perf_counter()
     e0.record(main)
     for st in strs[1:]:
@@ -175,24 +254,22 @@ def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1, sync_e
     for i in range(steps):
         launch(i, sps[i % streams])
         if sync_every and (i + 1) % sync_every == 0 and i + 1 < steps:
-            torch.cuda.synchronize()  # host waits for the queue to drain (inside the timed region)
+            torch.cuda.synchronize()
     for st, end in zip(strs[1:], ends[1:]):
         end.record(st)
         main.wait_event(end)
     e1.record(main)
     torch.cuda.synchronize()
+    barrier(world)
     t1 = time.perf_counter()
-    if world > 1:
-        torch.distributed.barrier()
     return t1 - t0, e0.elapsed_time(e1) / steps
 
 
 def time_graph(launch, steps, per_graph=100, spinup_ms=100.0):
     """The same launches replayed from a HIP graph: `per_graph` consecutive launches (rotating
     input sets) are stream-captured once (torch.cuda.graph), then the graph is replayed
-    steps / per_graph times between one hipEvent pair -- the host issues one graph launch per
-    `per_graph` steps instead of one C-ABI call per step, which is what a short kernel (a
-    65536-configuration batch runs ~4 us) needs.  Returns (wall s, device ms per step)."""
+    ceil(steps / per_graph) times between one hipEvent pair.
+    Returns (wall s, device ms per launch, launches replayed)."""
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):  # JIT compile + warm outside the capture
@@ -211,7 +288,7 @@ def time_graph(launch, steps, per_graph=100, spinup_ms=100.0):
     while (time.perf_counter() - t_spin) * 1e3 < spinup_ms:
         g.replay()
         torch.cuda.synchronize()
-    reps = max(1, steps // per_graph)
+    reps = max(1, -(-steps // per_graph))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -222,52 +299,36 @@ def time_graph(launch, steps, per_graph=100, spinup_ms=100.0):
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     del g
-    return t1 - t0, e0.elapsed_time(e1) / (reps * per_graph)
+    launches = reps * per_graph
+    return t1 - t0, e0.elapsed_time(e1) / launches, launches
 
 
 def batch_launcher(mb, sets, kernel, dtype, layout="soa", B=None):
-    """Closure issuing the batched entry point(s) of `kernel` on input set i % len(sets)."""
+    """Closure issuing the batched C-ABI entry point(s) of `kernel` on input set i % len(sets)."""
     lib = ffi.lib()
     suffix = "f32" if dtype == torch.float32 else "f64"
     ns = len(sets)
     if layout == "tiled":
-        rnea_t = getattr(lib, f"multibody_rnea_batch_tiled_{suffix}")
-        fd_t = getattr(lib, f"multibody_fd_batch_tiled_{suffix}")
-        calls = []
-        for i, o in sets:
-            p = [t.data_ptr() for t in i] + [t.data_ptr() for t in o]
-            if kernel == "rnea_fd":
-                calls.append(((rnea_t, (mb.handle, p[0], p[1], p[2], p[3], B)),
-                              (fd_t, (mb.handle, p[0], p[1], p[3], p[4], B))))
-            else:
-                calls.append(((rnea_t if kernel == "rnea" else fd_t, (mb.handle, p[0], p[1], p[2], p[3], B)),))
-
-        def launch_t(i, sp):
-            for fn, a in calls[i % ns]:
-                if fn(*a, sp):
-                    raise RuntimeError(ffi.last_error())
-
-        return launch_t
-    rnea = getattr(lib, f"multibody_rnea_batch_{suffix}")
-    fd = getattr(lib, f"multibody_fd_batch_{suffix}")
-    B = sets[0][1][0].shape[1]
-    ld = sets[0][1][0].stride(0) if sets[0][1][0].shape[0] > 1 else B
-    if kernel == "rnea_fd":
-        args = [((mb.handle, i[0].data_ptr(), i[1].data_ptr(), i[2].data_ptr(), o[0].data_ptr(), B, ld),
-                 (mb.handle, i[0].data_ptr(), i[1].data_ptr(), o[0].data_ptr(), o[1].data_ptr(), B, ld))
-                for i, o in sets]
-
-        def launch(i, sp):
-            a1, a2 = args[i % ns]
-            if rnea(*a1, sp) or fd(*a2, sp):
-                raise RuntimeError(ffi.last_error())
+        rnea = getattr(lib, f"multibody_rnea_batch_tiled_{suffix}")
+        fd = getattr(lib, f"multibody_fd_batch_tiled_{suffix}")
+        tail = (B,)
     else:
-        fn = rnea if kernel == "rnea" else fd
-        args = [(mb.handle, i[0].data_ptr(), i[1].data_ptr(), i[2].data_ptr(), o[0].data_ptr(), B, ld)
-                for i, o in sets]
+        rnea = getattr(lib, f"multibody_rnea_batch_{suffix}")
+        fd = getattr(lib, f"multibody_fd_batch_{suffix}")
+        B = sets[0][1][0].shape[1]
+        tail = (B, B)
+    calls = []
+    for i, o in sets:
+        p = [t.data_ptr() for t in i] + [t.data_ptr() for t in o]
+        if kernel == "rnea_fd":
+            calls.append(((rnea, (mb.handle, p[0], p[1], p[2], p[3]) + tail),
+                          (fd, (mb.handle, p[0], p[1], p[3], p[4]) + tail)))
+        else:
+            calls.append(((rnea if kernel == "rnea" else fd, (mb.handle, p[0], p[1], p[2], p[3]) + tail),))
 
-        def launch(i, sp):
-            if fn(*args[i % ns], sp):
+    def launch(i, sp):
+        for fn, args in calls[i % ns]:
+            if fn(*args, sp):
                 raise RuntimeError(ffi.last_error())
 
     return launch
@@ -289,48 +350,54 @@ def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED):
     args = (mb.handle, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), dt, K, None, B, B)
 
     def launch(i, sp):
-        rc = fn(*args, sp)
-        if rc:
+        if fn(*args, sp):
             raise RuntimeError(ffi.last_error())
 
     launch.keep = (q, qd, tau)
     return launch
 
 
-def run_timed(mb, sets, kernel, dtype, steps, warmup, world, spinup_ms=0.0, streams=1, layout="soa", B=None,
-              sync_every=0):
-    return time_launches(batch_launcher(mb, sets, kernel, dtype, layout, B), steps, warmup, world, spinup_ms, streams,
-                         sync_every)
+def measure(mb, kernel, dt_name, B, layout, steps, warmup, world, rotate_gib, seed, spinup_ms=300.0, streams=1,
+            sync_every=0, graph=False):
+    """Time `steps` launches of `kernel` over batches of B resident configurations.
+    Returns a dict (wall, kernel_ms_avg, bytes, sets) plus the graph-replay figures if asked."""
+    ds = DT[dt_name]
+    es = 4 if dt_name == "f32" else 8
+    ns = nsets_for(mb.n, B, es, kernel, rotate_gib)
+    sets = make_sets(mb, B, ds, kernel, ns, seed, layout=layout)
+    launch = batch_launcher(mb, sets, kernel, ds, layout, B)
+    wall, km = time_launches(launch, steps, warmup, world, spinup_ms, streams, sync_every)
+    r = {"wall": wall, "kernel_ms_avg": km, "bytes": set_bytes(mb.n, B, es, kernel), "sets": ns}
+    if graph:
+        gw, gkm, gl = time_graph(launch, steps)
+        r.update({"graph_wall": gw, "graph_kernel_ms_avg": gkm, "graph_launches": gl})
+    del sets, launch
+    torch.cuda.empty_cache()
+    return r
 
 
-def side_workloads(mb7, a, rotate_gib):
+def side_workloads(mb7, a):
     """Secondary measurements (one GPU, serial launches): the other SURVEY §8(d) configs."""
     sec = {}
     steps = max(20, a.steps // 4)
 
-    def one(name, mb, kernel, dt_name, B=a.batch, graph=False):
-        ds = DT[dt_name]
-        es = 4 if dt_name == "f32" else 8
-        per = set_bytes(mb.n, B, es, kernel)
-        sets = make_sets(mb, B, ds, kernel, max(2, int(np.ceil(rotate_gib * (1 << 30) / per))), chains.SEED + 31,
-                         layout=a.layout)
-        w, km = run_timed(mb, sets, kernel, ds, steps, 5, 1, 300.0, 1, a.layout, B)
-        sec[name] = {"evals_per_s": B * steps / w, "kernel_ms_avg": km, "batch": B, "layout": a.layout,
-                     "hbm_frac": per / (km * 1e-3) / HBM_PEAK,
+    def one(name, mb, kernel, dt_name, B=a.batch, layout=a.layout, graph=False):
+        r = measure(mb, kernel, dt_name, B, layout, steps, 5, 1, a.rotate_gib, chains.SEED + 31, graph=graph)
+        sec[name] = {"evals_per_s": B * steps / r["wall"], "kernel_ms_avg": r["kernel_ms_avg"], "batch": B,
+                     "layout": layout, "dtype": dt_name, "hbm_frac": r["bytes"] / (r["kernel_ms_avg"] * 1e-3) / HBM_PEAK,
                      "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64") for k in kernel.split("_"))}
-        if graph:  # the same launches replayed from a HIP graph
-            gw, gkm = time_graph(batch_launcher(mb, sets, kernel, ds, a.layout, B), steps)
-            sec[name + "_graph"] = {"evals_per_s": B * steps / gw, "kernel_ms_avg": gkm, "batch": B,
-                                    "layout": a.layout, "hbm_frac": per / (gkm * 1e-3) / HBM_PEAK,
+        if graph:  # the same launches replayed from a HIP graph; rates over the launches replayed
+            gl = r["graph_launches"]
+            sec[name + "_graph"] = {"evals_per_s": B * gl / r["graph_wall"],
+                                    "kernel_ms_avg": r["graph_kernel_ms_avg"], "batch": B, "layout": layout,
+                                    "dtype": dt_name, "launches": gl,
+                                    "hbm_frac": r["bytes"] / (r["graph_kernel_ms_avg"] * 1e-3) / HBM_PEAK,
                                     "launch": "HIP graph of 100 captured C-ABI launches, replayed"}
-        del sets
-        torch.cuda.empty_cache()
 
     one("rnea_fr3_f32_b65536", mb7, "rnea", "f32", 65536, graph=True)    # config 2
     one("fd_fr3_f32_b65536", mb7, "fd", "f32", 65536, graph=True)        # config 3
-    one("rnea_fr3_f64", mb7, "rnea", "f64")
-    one("fd_fr3_f32", mb7, "fd", "f32")
     one("fd_fr3_f64", mb7, "fd", "f64")
+    one("fd_fr3_f32", mb7, "fd", "f32")
     one("rnea_fd_fr3_f64_b131072", mb7, "rnea_fd", "f64", 1 << 17, graph=True)  # config 4, one GPU's 2^17 shard
     mb30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     mb30.upload()
@@ -341,7 +408,6 @@ def side_workloads(mb7, a, rotate_gib):
     one("rnea_float14_tree_f32", mbt, "rnea", "f32")
     one("fd_float14_tree_f32", mbt, "fd", "f32")
     # fused rollout: K forward-dynamics + Euler steps per launch
-    # (its clock settles only after ~150 ms of this VALU-dense load: 495 -> 357 us per launch)
     K, nl = 16, 40
     w, km = time_launches(rollout_launcher(mb7, a.batch, torch.float32, K), nl, 3, 1, 300.0)
     sec["rollout_fr3_f32_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
@@ -350,7 +416,31 @@ def side_workloads(mb7, a, rotate_gib):
     return sec
 
 
-def cpu_baseline(n, B_sample_hint, kernel, cpu_seconds):
+def single_call(iters=2000):
+    """latency of the reference's single-configuration ABI calls
+    (multibody_rnea / _crba / _jac / _fwd_kin, rigidbody_bindings/src/lib.rs:15-70) as the C++
+    consumer main.cpp:69-96 times them -- examples/single_call_bench.cpp, a child process
+    linked against librigidbody_bindings.so."""
+    exe = os.path.join(REPO, "rigidbody-rs_amd", "bin", "single_call_bench")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} not built (make -C rigidbody-rs_amd)"}
+    r = subprocess.run([exe, str(iters)], capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return {"error": r.stderr[-500:]}
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res["how"] = ("C++ consumer (examples/single_call_bench.cpp), std::chrono around each call on the "
+                  "main.cpp:103-105 input after 50 warm calls; every call = H2D, kernel, D2H, stream sync")
+    return res
+
+
+def host_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(n, kernel, cpu_seconds):
     """fp64 CPU restatement (oracle/, kind "port") timed on this host's cores."""
     from oracle import oracle, urdf_model
 
@@ -358,11 +448,9 @@ def cpu_baseline(n, B_sample_hint, kernel, cpu_seconds):
     xml = chains.fr3_urdf_text() if n == 7 else chains.synthetic_chain_urdf(n)
     raw = urdf_model.model_raw_from_urdf(xml)
     om = oracle.Model(raw)
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(16, cores))  # the GPU box's CPU share is 16
+    visible = host_cores()
+    # the GPU box's CPU share is 16 (os.cpu_count() there shows the whole machine)
+    cores = max(1, min(16, visible))
     mbl = ([l["lower"] for l in raw["limits"]], [l["upper"] for l in raw["limits"]],
            [l["velocity"] for l in raw["limits"]], [l["effort"] for l in raw["limits"]])
     kinds = ("q", "qd", "tau") if kernel == "fd" else ("q", "qd", "qdd")
@@ -380,14 +468,21 @@ def cpu_baseline(n, B_sample_hint, kernel, cpu_seconds):
     t = time.perf_counter()
     call(*cal, nthreads=1)
     rate1 = 20000 / (time.perf_counter() - t)
+    t = time.perf_counter()
+    om.crba_batch(cal[0], nthreads=1)
+    crba1 = 20000 / (time.perf_counter() - t)
     sample = int(min(max(rate1 * cpu_seconds, 1e5), 5e7))
     x = inputs(sample)
     t = time.perf_counter()
     call(*x, nthreads=cores)
     dt = time.perf_counter() - t
     return {"value": sample / dt, "unit": "evals/s", "cores": cores, "kind": "port",
-            "sample": f"{sample} fr3 configs (same distributions/seed as the GPU run), fp64 oracle "
-                      f"{kernel} over {cores} OpenMP threads, {dt:.2f} s wall; single-thread {rate1:.3g} evals/s"}
+            "host_cpus_visible": visible, "nproc": os.cpu_count(),
+            "single_thread_evals_per_s": rate1, "single_thread_us_per_call": 1e6 / rate1,
+            "single_thread_crba_us_per_call": 1e6 / crba1,
+            "sample": f"{sample} {'fr3' if n == 7 else f'chain{n}'} configs (same distributions/seed as the GPU run), "
+                      f"fp64 oracle {kernel} over {cores} OpenMP threads (of {visible} visible CPUs, cap 16 = the "
+                      f"GPU box's CPU share), {dt:.2f} s wall; single-thread {rate1:.3g} evals/s"}
 
 
 def load_traffic(workload):
@@ -398,28 +493,39 @@ def load_traffic(workload):
     return None
 
 
-def main():
-    a = parse()
-    world, rank, local = init_dist()
+def workload_name(kernel, n, dt_name, layout, B):
+    return f"{kernel}_{'fr3' if n == 7 else f'chain{n}'}_{dt_name}_{layout}_b{B}"
+
+
+def main(a):
+    world, rank, dev = init_dist(a)
     n = a.dof
-    dtype = DT[a.dtype]
     esize = 4 if a.dtype == "f32" else 8
-    mb = load_model(world, rank, n)
-    per_set = set_bytes(n, a.batch, esize, a.kernel)
-    nsets = max(2, int(np.ceil(a.rotate_gib * (1 << 30) / per_set)))
-    sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, rdist.rank_seed(chains.SEED, rank), layout=a.layout)
-    wall, kern_avg_ms = run_timed(mb, sets, a.kernel, dtype, a.steps, a.warmup, world, a.spinup_ms, a.streams,
-                                  a.layout, a.batch, a.sync_every)
-    wall, kern_avg_ms = rdist.max_over_ranks([wall, kern_avg_ms], world, torch.device("cuda"))
-    evals = world * a.batch * a.steps
-    value = evals / wall
-    # q, qd, qdd|tau read + tau|qdd written per kernel; rnea_fd counts both
+    mb = load_model(world, rank, n, dev)
+    strong = a.split == "strong"
+    lo, hi = rdist.shard(a.batch, rank, world) if strong else (0, a.batch)
+    B = hi - lo  # this rank's configurations per step
+    global_batch = a.batch if strong else a.batch * world
+    seed = chains.SEED if strong else rdist.rank_seed(chains.SEED, rank)
+    if a.stub:
+        # plumbing rehearsal: same ranks, collectives and reporting, no device work
+        t0 = time.perf_counter()
+        barrier(world)
+        wall = time.perf_counter() - t0 + 1e-9
+        r = {"wall": wall, "kernel_ms_avg": wall / a.steps * 1e3, "bytes": set_bytes(n, B, esize, a.kernel), "sets": 0}
+        kpath = "stub"
+    else:
+        r = measure(mb, a.kernel, a.dtype, B, a.layout, a.steps, a.warmup, world, a.rotate_gib, seed, a.spinup_ms,
+                    a.streams, a.sync_every)
+        kpath = "+".join(mb.kernel_path(k, a.dtype == "f64") for k in a.kernel.split("_"))
+    wall, kern_ms = rdist.max_over_ranks([r["wall"], r["kernel_ms_avg"]], world, dev)
+    value = global_batch * a.steps / wall
     bytes_per_eval = set_bytes(n, 1, esize, a.kernel)
-    achieved = bytes_per_eval * a.batch / (kern_avg_ms * 1e-3)
-    workload = f"{a.kernel}_{'fr3' if n == 7 else f'chain{n}'}_{a.dtype}_{a.layout}_b{a.batch}"
-    traffic = load_traffic(workload)
+    achieved = bytes_per_eval * B / (kern_ms * 1e-3)
+    workload = workload_name(a.kernel, n, a.dtype, a.layout, a.batch)
+    traffic = load_traffic(workload) if not strong else None
     line = {
-        "metric": "RNEA evals/sec (fr3 7-DOF, batch 2^20) at 1/2/4/8 MI355X; % HBM roofline",
+        "metric": METRIC,
         "value": value,
         "unit": "evals/s",
         "n_gpus": world,
@@ -427,43 +533,62 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": wall / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": a.dtype,
-        "data": "synthetic (device splitmix64, SURVEY.md §8(d) distributions, seed 20250224)",
+        "data": ("stub (CPU rehearsal of the rank plumbing, no kernels)" if a.stub else
+                 "synthetic (device splitmix64, SURVEY.md §8(d) distributions, seed 20250224)"),
         "config": {"workload": workload, "kernel": a.kernel, "model": "fr3 7-DOF" if n == 7 else f"chain{n}",
                    "layout": ("tiled [B/256][n][256] (each 256-configuration tile of all joints contiguous)"
                               if a.layout == "tiled" else "SoA rows [n][B]"),
-                   "streams": a.streams,
-                   "batch_per_gpu": a.batch, "global_batch": a.batch * world, "dof": n,
-                   "parallelism": f"dp{world} (independent shards, RCCL model broadcast)",
-                   "input_sets": nsets, "rotated_bytes": nsets * per_set,
-                   "kernel_path": "+".join(mb.kernel_path(k, a.dtype == "f64") for k in a.kernel.split("_"))},
+                   "streams": a.streams, "split": a.split,
+                   "batch_per_gpu": B, "global_batch": global_batch, "dof": n,
+                   "parallelism": f"dp{world} ({a.split} split; independent shards, RCCL model broadcast)",
+                   "input_sets": r["sets"], "rotated_bytes": r["sets"] * r["bytes"], "kernel_path": kpath},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,
-                     "bytes_per_eval": bytes_per_eval, "evals_per_launch": a.batch, "kernel_ms_avg": kern_avg_ms,
+                     "bytes_per_eval": bytes_per_eval, "evals_per_launch": B, "kernel_ms_avg": kern_ms,
                      "timing": (f"kernel_ms_avg = hipEvent pair on the launch stream around the {a.steps} timed "
-                                f"launches / {a.steps} ({a.streams} stream(s); includes the inter-launch gap)")},
+                                f"launches / {a.steps} ({a.streams} stream(s); includes the inter-launch gap); "
+                                "max over ranks")},
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(n, a.batch, a.kernel, a.cpu_seconds)
-    if rank == 0 and not a.no_secondary and world == 1 and n == 7:
-        # the same workload with consecutive batches overlapped on 2 streams
-        w2, k2 = run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 50.0, 2, a.layout, a.batch)
-        sec = {f"{a.kernel}_{a.dtype}_{a.layout}_2streams": {
-            "evals_per_s": a.batch * a.steps / w2, "step_ms_device": k2,
-            "hbm_frac_effective": bytes_per_eval * a.batch / (k2 * 1e-3) / HBM_PEAK}}
-        del sets
-        torch.cuda.empty_cache()
-        if a.layout != "soa":  # the same workload on plain SoA rows
-            sets = make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED + 7)
-            w3, k3 = run_timed(mb, sets, a.kernel, dtype, a.steps, 5, 1, 100.0)
-            sec[f"{a.kernel}_{a.dtype}_soa"] = {"evals_per_s": a.batch * a.steps / w3, "kernel_ms_avg": k3,
-                                                "hbm_frac": bytes_per_eval * a.batch / (k3 * 1e-3) / HBM_PEAK}
-            del sets
-            torch.cuda.empty_cache()
-        sec.update(side_workloads(mb, a, a.rotate_gib))
+    if traffic:
+        line["roofline"]["traffic_source"] = f"profiles/traffic_{workload}.json (rocprofv3 PMC passes)"
+    sec = {}
+    if world > 1 and not strong and not a.stub:
+        # the same global 2^20 batch sharded across the ranks, beside the weak line
+        slo, shi = rdist.shard(a.batch, rank, world)
+        rs = measure(mb, a.kernel, a.dtype, shi - slo, a.layout, a.steps, 5, world, a.rotate_gib, chains.SEED, 100.0)
+        sw, sk = rdist.max_over_ranks([rs["wall"], rs["kernel_ms_avg"]], world, dev)
+        sec["strong_split"] = {"evals_per_s": a.batch * a.steps / sw, "global_batch": a.batch,
+                               "batch_per_gpu_max": -(-a.batch // world), "ms_per_step": sw / a.steps * 1e3,
+                               "kernel_ms_avg_max_rank": sk, "scaling": "strong"}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.stub:
+        line["cpu_baseline"] = cpu_baseline(n, a.kernel, a.cpu_seconds)
+    if rank == 0 and not a.no_secondary and world == 1 and n == 7 and not a.stub:
+        steps = a.steps
+        r2 = measure(mb, a.kernel, a.dtype, a.batch, a.layout, steps, 5, 1, a.rotate_gib, seed, 50.0, 2)
+        sec[f"{a.kernel}_{a.dtype}_{a.layout}_2streams"] = {
+            "evals_per_s": a.batch * steps / r2["wall"], "step_ms_device": r2["kernel_ms_avg"],
+            "hbm_frac_effective": r2["bytes"] / (r2["kernel_ms_avg"] * 1e-3) / HBM_PEAK}
+        # the comparable SoA line (north_star's layout) and the reduced-precision fp32 variant
+        other = "f32" if a.dtype == "f64" else "f64"
+        for dt_name, layout in ((a.dtype, "soa"), (other, a.layout), (other, "soa")):
+            if layout == a.layout and dt_name == a.dtype:
+                continue
+            rr = measure(mb, a.kernel, dt_name, a.batch, layout, steps, 5, 1, a.rotate_gib, seed + 7, 100.0)
+            sec[workload_name(a.kernel, n, dt_name, layout, a.batch)] = {
+                "evals_per_s": a.batch * steps / rr["wall"], "kernel_ms_avg": rr["kernel_ms_avg"],
+                "hbm_frac": rr["bytes"] / (rr["kernel_ms_avg"] * 1e-3) / HBM_PEAK, "dtype": dt_name,
+                "layout": layout, "note": "reduced precision (the reference computes in f64)" if dt_name == "f32" else ""}
+        sec.update(side_workloads(mb, a))
+        sec["single_call"] = single_call()
+        if "cpu_baseline" in line:
+            cb = line["cpu_baseline"]
+            sec["single_call"]["oracle_single_thread_us"] = {"rnea": cb["single_thread_us_per_call"],
+                                                             "crba": cb["single_thread_crba_us_per_call"]}
+    if sec:
         line["secondary"] = sec
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -472,4 +597,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(_ARGS)

@@ -1,0 +1,57 @@
+"""bench.py's multi-rank launch on CPU: `--gpus N` started by hand spawns N ranks itself
+(the parent never touches a GPU), every rank joins one process group of size N, and exactly
+one JSON line comes back -- the driver's `python bench.py --gpus N` contract.  --stub runs
+the same spawning, rank setup, model broadcast, shard split, max-over-ranks reduction and
+reporting over gloo with no kernels."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+
+def _run(*args, env=None):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--stub", "--steps", "5", "--warmup", "0",
+                        *args], capture_output=True, text=True, timeout=300, env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("split", ["weak", "strong"])
+def test_gpus2_spawns_two_ranks(split):
+    line = _run("--gpus", "2", "--split", split)
+    assert line["n_gpus"] == 2
+    assert line["scaling"] == split
+    cfg = line["config"]
+    if split == "weak":
+        assert cfg["global_batch"] == 2 * (1 << 20) and cfg["batch_per_gpu"] == 1 << 20
+    else:
+        assert cfg["global_batch"] == 1 << 20 and cfg["batch_per_gpu"] == 1 << 19
+    assert line["value"] > 0 and line["metric"].startswith("RNEA evals/sec")
+    assert line["dtype"] == "f64"  # the reference's Real (lib.rs:15)
+
+
+def test_single_rank_default():
+    line = _run()
+    assert line["n_gpus"] == 1 and line["scaling"] == "weak"
+    assert line["config"]["workload"] == "rnea_fr3_f64_tiled_b1048576"
+
+
+def test_failed_rank_fails_the_job():
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    # an impossible model size makes every rank raise before the process group forms
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--stub", "--gpus", "2", "--dof", "9999",
+                        "--steps", "1"], capture_output=True, text=True, timeout=300, env=e)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

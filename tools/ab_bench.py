@@ -30,8 +30,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--rollout-k", type=int, default=16, help="steps per launch for --kernel rollout")
     ap.add_argument("--layouts", nargs="+", default=["soa"], choices=["soa", "tiled"])
-    ap.add_argument("--pads", type=int, nargs="+", default=[0],
-                    help="leading-dimension paddings (elements) to compare; each becomes its own input sets")
     ap.add_argument("--variants", nargs="+", default=["rnea_stream=0", "rnea_stream=1"],
                     help="comma-separated rb_set_tuning key=value lists; the pseudo-key 'streams' "
                          "sets how many HIP streams the timed launches rotate over")
@@ -44,12 +42,11 @@ def main():
     nsets = max(2, int(np.ceil(1.25 * (1 << 30) / per)))
     launches = {}
     for lay in a.layouts:
-        for pad in a.pads:
-            if a.kernel == "rollout":
-                launches[(lay, pad)] = bench.rollout_launcher(mb, a.batch, dtype, a.rollout_k)
-            else:
-                sets = bench.make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED, pad, lay)
-                launches[(lay, pad)] = bench.batch_launcher(mb, sets, a.kernel, dtype, lay, a.batch)
+        if a.kernel == "rollout":
+            launches[lay] = bench.rollout_launcher(mb, a.batch, dtype, a.rollout_k)
+        else:
+            sets = bench.make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED, lay)
+            launches[lay] = bench.batch_launcher(mb, sets, a.kernel, dtype, lay, a.batch)
     lib = ffi.lib()
     # every knob any variant sets is reset to the library default (tuning.hpp) before each
     # variant, so a knob of one variant never leaks into the next
@@ -60,7 +57,7 @@ def main():
     keys = [(v, lp) for v in a.variants for lp in launches]
     res = {k: [] for k in keys}
     for r in range(a.rounds):
-        for v, pad in keys:
+        for v, lay in keys:
             nstreams = 1
             for k in used:
                 assert lib.rb_set_tuning(k.encode(), defaults[k]) == 0, ffi.last_error()
@@ -70,12 +67,11 @@ def main():
                     nstreams = int(val)
                     continue
                 assert lib.rb_set_tuning(k.encode(), int(val)) == 0, ffi.last_error()
-            _, ms = bench.time_launches(launches[pad], a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
-            res[(v, pad)].append(ms)  # pad = (layout, pad) key
+            _, ms = bench.time_launches(launches[lay], a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
+            res[(v, lay)].append(ms)
     out = {}
-    for (v, pad), ms in res.items():
-        lay, pd = pad
-        v = v + ("" if len(a.pads) == 1 else f",pad={pd}") + ("" if len(a.layouts) == 1 else f",{lay}")
+    for (v, lay), ms in res.items():
+        v = v + ("" if len(a.layouts) == 1 else f",{lay}")
         med = float(np.median(ms))
         out[v] = {"ms_median": med, "ms_min": float(np.min(ms)), "ms_rounds": [float(x) for x in ms],
                   "evals_per_s": a.batch / (med * 1e-3),

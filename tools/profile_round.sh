@@ -1,18 +1,23 @@
 #!/bin/bash
-# GPU-box recipe for the round's committed profiles: the default bench line, a kernel
-# trace (--kernel-trace --stats) of the headline command (its own printed bench line is
-# checked against its trace by tools/trace_check.py), and four separate PMC passes.
-# Each step is time-limited; the chain stops at the first failure.
-# usage (via gpurun): tools/profile_round.sh
+# GPU-box recipe for committed profiles of one bench workload: a kernel trace
+# (--kernel-trace --stats) of the bench command itself (its own printed bench line is checked
+# against its trace by tools/trace_check.py) and four separate PMC passes (FETCH_SIZE and
+# WRITE_SIZE cannot share a pass; SQ and GRBM counters in their own).  Each step is
+# time-limited; the chain stops at the first fault / timeout (tools/gpu_steps.sh).
+#
+# usage (via gpurun): tools/profile_round.sh TAG [bench.py args...]
+#   outputs under gpurun_out/TAG/{trace,pmc_fetch,pmc_write,pmc_sq,pmc_grbm} + TAG_*.log
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 R=$PWD
-O=$R/gpurun_out
-HEAD="python3 $R/bench.py --no-cpu-baseline --no-secondary"
+TAG=${1:?usage: profile_round.sh TAG [bench args]}
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+B="python3 $R/bench.py --no-cpu-baseline --no-secondary $*"
 export TMPDIR=/tmp
 tools/gpu_steps.sh \
-  bench 400 "python bench.py" \
-  trace 300 "cd /tmp && rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $HEAD" \
-  pmc_fetch 300 "cd /tmp && rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $HEAD" \
-  pmc_write 300 "cd /tmp && rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $HEAD" \
-  pmc_sq 300 "cd /tmp && rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $O/pmc_sq -o run --output-format csv -- $HEAD" \
-  pmc_grbm 300 "cd /tmp && rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS -d $O/pmc_grbm -o run --output-format csv -- $HEAD"
+  "${TAG}_trace" 300 "cd /tmp && rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B" \
+  "${TAG}_pmc_fetch" 300 "cd /tmp && rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $B" \
+  "${TAG}_pmc_write" 300 "cd /tmp && rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $B" \
+  "${TAG}_pmc_sq" 300 "cd /tmp && rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $O/pmc_sq -o run --output-format csv -- $B" \
+  "${TAG}_pmc_grbm" 300 "cd /tmp && rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS -d $O/pmc_grbm -o run --output-format csv -- $B"

@@ -3,7 +3,8 @@ process (tools/profile_round.sh `trace` step): the headline JSON line that proce
 the mean duration of the last `steps` headline-kernel dispatches in its kernel trace (the
 timed region), plus the idle gap between them.
 
-usage: python tools/trace_check.py GPURUN_OUT_DIR OUT_JSON
+usage: python tools/trace_check.py BENCH_LOG TRACE_DIR OUT_JSON
+  (tools/profile_round.sh TAG: gpurun_out/TAG_trace.log and gpurun_out/TAG/trace)
 """
 import csv
 import glob
@@ -13,14 +14,14 @@ import sys
 
 
 def main():
-    d, out = sys.argv[1], sys.argv[2]
+    log, tdir, out = sys.argv[1], sys.argv[2], sys.argv[3]
     line = None
-    for ln in open(os.path.join(d, "trace.log")):
+    for ln in open(log):
         ln = ln.strip()
         if ln.startswith("{") and '"metric"' in ln:
             line = json.loads(ln)
     steps = line["steps"]
-    f = glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))[0]
+    f = glob.glob(os.path.join(tdir, "*kernel_trace.csv"))[0]
     rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
                   for r in csv.DictReader(open(f)) if r["Kernel_Name"] == "rb_jit_kernel")
     timed = rows[-steps:]

@@ -18,7 +18,7 @@ import os
 import sys
 
 
-def load(d, regex):
+def load(d, regex, durations=None):
     import re
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = {}
@@ -26,6 +26,8 @@ def load(d, regex):
         for r in csv.DictReader(open(f)):
             if re.search(regex, r["Kernel_Name"]):
                 vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+                if durations is not None and r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                    durations.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     return vals
 
 
@@ -34,8 +36,12 @@ def main():
     regex = sys.argv[4] if len(sys.argv) > 4 else "rb_jit_kernel"
     os.makedirs(prof, exist_ok=True)
     per = {}
+    durs = []
+    grbm = []
     for p in ("fetch", "write", "sq", "grbm"):
-        v = load(os.path.join(src, f"pmc_{p}"), regex)
+        v = load(os.path.join(src, f"pmc_{p}"), regex, durs if p == "grbm" else None)
+        if p == "grbm":
+            grbm = v.get("GRBM_GUI_ACTIVE", [])
         if not v:
             continue
         with open(os.path.join(prof, f"pmc_{p}_summary.csv"), "w", newline="") as f:
@@ -46,14 +52,35 @@ def main():
                 per[k] = sum(xs) / len(xs)
     n, B = 7, int(workload.rsplit("_b", 1)[1])
     es = 4 if "_f32_" in workload else 8
-    alg = 4 * n * es * B
-    out = {"workload": workload, "kernel": f"{regex} (model-specialised RNEA)",
+    alg = (8 if workload.startswith("rnea_fd") else 4) * n * es * B
+    kind = workload.split("_")[0]
+    out = {"workload": workload, "kernel": f"{regex} (model-specialised {kind.upper()})",
            "algorithmic_bytes_per_launch": alg}
     if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
         hbm = 2 * per["FETCH_SIZE"] * 1024 + per["WRITE_SIZE"] * 1024
         out.update({"bytes_per_launch": hbm, "traffic_over_algorithmic": hbm / alg,
                     "FETCH_SIZE_KB_per_launch": per["FETCH_SIZE"], "WRITE_SIZE_KB_per_launch": per["WRITE_SIZE"]})
-    out["sq_counters_per_launch"] = {k: v for k, v in per.items() if k.startswith("SQ_")}
+    sq = {k: v for k, v in per.items() if k.startswith("SQ_")}
+    out["sq_counters_per_launch"] = sq
+    if "SQ_WAVE_CYCLES" in sq and sq["SQ_WAVE_CYCLES"] > 0:
+        # quad-cycle counters (MI355X_MICROARCH.md): fractions of the waves' lifetime
+        wc = sq["SQ_WAVE_CYCLES"]
+        out["wave_time_fractions"] = {k.replace("SQ_", "").lower(): sq[k] / wc for k in
+                                      ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")
+                                      if k in sq}
+        if "SQ_WAVES" in sq:
+            out["valu_insts_per_wave"] = sq.get("SQ_INSTS_VALU", 0) / sq["SQ_WAVES"]
+    if grbm and durs:
+        # GRBM_GUI_ACTIVE per ns of the (serialised, profiled) dispatch: a relative clock /
+        # busy measure per launch window; the per-eighth profile attributes slow phases
+        k = max(1, len(grbm) // 8)
+        rate = [g / d for g, d in zip(grbm, durs)]
+        out["grbm_gui_active_per_ns"] = {
+            "mean": sum(rate) / len(rate),
+            "by_eighth": [round(sum(rate[i:i + k]) / len(rate[i:i + k]), 3) for i in range(0, len(rate), k)],
+            "dispatch_ns_by_eighth": [round(sum(durs[i:i + k]) / len(durs[i:i + k]), 1) for i in range(0, len(durs), k)],
+            "note": "GRBM_GUI_ACTIVE / (End - Start) of the PMC pass's dispatches (counter summed over the "
+                    "chip's GRBM instances, so a relative figure, not MHz)"}
     out["grbm_per_launch"] = {k: v for k, v in per.items() if k.startswith("GRBM_")}
     out["method"] = ("rocprofv3 --pmc passes FETCH_SIZE / WRITE_SIZE / SQ_* / GRBM_* run separately on "
                      "`bench.py --no-cpu-baseline --no-secondary`, kernels matching " + regex +
