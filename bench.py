@@ -420,17 +420,24 @@ def single_call(iters=2000):
     """latency of the reference's single-configuration ABI calls
     (multibody_rnea / _crba / _jac / _fwd_kin, rigidbody_bindings/src/lib.rs:15-70) as the C++
     consumer main.cpp:69-96 times them -- examples/single_call_bench.cpp, a child process
-    linked against librigidbody_bindings.so."""
+    linked against librigidbody_bindings.so.  Two runs: the default dispatch (the calling
+    thread evaluates the GPU lane bodies compiled for the host, host_eval.cpp) and
+    RB_SINGLE_GPU=1 (every call a GPU round trip: H2D, kernel, D2H, stream sync)."""
     exe = os.path.join(REPO, "rigidbody-rs_amd", "bin", "single_call_bench")
     if not os.path.exists(exe):
         return {"error": f"{exe} not built (make -C rigidbody-rs_amd)"}
-    r = subprocess.run([exe, str(iters)], capture_output=True, text=True, timeout=300)
-    if r.returncode != 0:
-        return {"error": r.stderr[-500:]}
-    res = json.loads(r.stdout.strip().splitlines()[-1])
-    res["how"] = ("C++ consumer (examples/single_call_bench.cpp), std::chrono around each call on the "
-                  "main.cpp:103-105 input after 50 warm calls; every call = H2D, kernel, D2H, stream sync")
-    return res
+    out = {}
+    for name, env in (("host", {}), ("gpu", {"RB_SINGLE_GPU": "1"})):
+        r = subprocess.run([exe, str(iters)], capture_output=True, text=True, timeout=300,
+                           env={**os.environ, **env})
+        if r.returncode != 0:
+            out[name] = {"error": r.stderr[-500:]}
+            continue
+        out[name] = json.loads(r.stdout.strip().splitlines()[-1])
+    out["how"] = ("C++ consumer (examples/single_call_bench.cpp), std::chrono around each call on the "
+                  "main.cpp:103-105 input after 50 warm calls, result buffer freed per call; 'host' = the "
+                  "default dispatch (lane bodies on the calling thread), 'gpu' = RB_SINGLE_GPU=1")
+    return out
 
 
 def host_cores():

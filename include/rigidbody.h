@@ -14,8 +14,11 @@
  * reference leaks Box::into_raw results, lib.rs:28,41,55,68); it is malloc'd, so
  * free() or multibody_result_free() (rigidbody_batch.h) releases it.
  *
- * All queries execute on the GPU (HIP, gfx950) in fp64; see rigidbody_batch.h for
- * the batched entry points that are the actual hot path.
+ * All queries compute in fp64.  One configuration per call is the reference's CPU use
+ * (main.cpp:69), so these run on the calling thread with the GPU kernels' own lane bodies
+ * compiled for the host (a GPU round trip per call would cost ~25x the recursion); models
+ * that need model-specialised kernels (trees) launch on the GPU.  The batched entry points
+ * of rigidbody_batch.h -- the actual hot path -- run on the GPU (HIP, gfx950) only.
  */
 #ifndef MULTIBODY_INTERFACE_H
 #define MULTIBODY_INTERFACE_H

@@ -111,6 +111,11 @@ int multibody_upload(const Multibody *mb);
  * rb_last_error() holds the log -- a tree model's calls then fail with RB_ERR_UNSUPPORTED). */
 int multibody_kernel_path(const Multibody *mb, int kind, int f64);
 int multibody_rnea_kernel_path(const Multibody *mb, int f64);
+/* Where the reference's single-configuration queries (rigidbody.h: rnea, crba, fwd_kin,
+ * jac) run for this model: 0 = on the calling host thread (the GPU lane bodies compiled for
+ * the host; serial revolute chains of a precompiled DOF on an FMA3/AVX2 CPU), 1 = one GPU
+ * launch per call (trees / prismatic joints, or rb_set_tuning("single_gpu", 1)). */
+int multibody_single_config_path(const Multibody *mb);
 /* The generated source of a model-specialised kernel (returns its length; copies at
  * most cap-1 bytes + NUL into buf when buf != NULL). */
 int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap);

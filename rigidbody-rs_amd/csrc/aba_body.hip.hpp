@@ -12,7 +12,7 @@ namespace rbamd {
 namespace dev {
 
 template <typename T, int N, bool FAST, typename Out>
-__device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
+RB_HD void aba_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
                                          Out &&out) {
     T cs[N], sn[N];
     T cw0[N], cw1[N], cv0[N], cv1[N];  // c_i = v_i x (S qd_i): (w.y qd, -w.x qd, 0; v.y qd, -v.x qd, 0)
@@ -125,7 +125,7 @@ __device__ __forceinline__ void aba_eval(const T *mdl, const T (&qv)[N], const T
 }
 
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-__device__ __forceinline__ void aba_any(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
+RB_HD void aba_any(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
                                         Out &&out) {
     if constexpr (Topo::kSerial)
         aba_eval<T, N, FAST>(mdl, qv, qdv, tv, static_cast<Out &&>(out));
@@ -179,53 +179,6 @@ __device__ __forceinline__ void aba_lane2(const f2 *mdl, const float *__restrict
         __builtin_amdgcn_sched_barrier(0);
     }
     aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 v) { st_row2(qdd, oA, oB, j * ld, off, v); });
-}
-
-// Resident grid-stride form (A/B, model-specialised kernels): each lane walks the batch
-// with stride gridDim.x * 256 and issues the NEXT configuration's q, qd, tau loads before
-// evaluating the current one, so a block's loads for configuration k+1 are in flight while it
-// computes k (21 VGPRs in fp32 FR3).  The current set is always older than the prefetch in
-// the in-order vmcnt queue, so its counted waits never wait for the prefetch.  Block k of
-// pass i covers configurations (k + i * gridDim.x) * 256 + [0, 256); the tiled / SoA block
-// base is o(b0) = (b0 / 256) * bs + b0 % 256 as in the lane kernels.
-template <typename T, int N, bool FAST, typename Topo = SerialTopo>
-__device__ __forceinline__ void aba_stream(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
-                                           const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
-                                           int64_t ld, int64_t bs) {
-    const uint32_t off = threadIdx.x * (uint32_t)sizeof(T);
-    uint32_t blk = blockIdx.x;
-    const uint32_t nblk = (B + 255u) / 256u;
-    auto base = [&](uint32_t k) { return (int64_t)k * bs; };
-    auto load = [&](uint32_t k, T (&x)[N], T (&y)[N], T (&z)[N]) {
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            x[j] = ld_row(q + base(k), j * ld, off);
-            y[j] = ld_row(qd + base(k), j * ld, off);
-        }
-#pragma unroll
-        for (int j = N - 1; j >= 0; --j) z[j] = ld_row(tau + base(k), j * ld, off);
-    };
-    T qv[N], qdv[N], tv[N];
-    bool live = blk < nblk && blk * 256u + threadIdx.x < B;
-    if (live) load(blk, qv, qdv, tv);
-    while (blk < nblk) {
-        const uint32_t nxt = blk + gridDim.x;
-        const bool nlive = nxt < nblk && nxt * 256u + threadIdx.x < B;
-        T nq[N], nqd[N], nt[N];
-        if (nlive) load(nxt, nq, nqd, nt);
-        if (live) {
-            T *out = qdd + base(blk);
-            aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T v) { st_row(out, j * ld, off, v); });
-        }
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            qv[j] = nq[j];
-            qdv[j] = nqd[j];
-            tv[j] = nt[j];
-        }
-        live = nlive;
-        blk = nxt;
-    }
 }
 
 // Fused rollout (the MPC-shooting use of forward dynamics): K steps

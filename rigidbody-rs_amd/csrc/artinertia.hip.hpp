@@ -17,7 +17,7 @@ struct ArtI {
 };
 
 template <typename T>
-__device__ __forceinline__ ArtI<T> rigid_inertia(const Link<T> &L) {
+RB_HD ArtI<T> rigid_inertia(const Link<T> &L) {
     // I_o, [h]x, m*1  (Inertia::to_matrix6 form, inertia.rs:53-70)
     ArtI<T> I;
     I.A = L.Io;
@@ -28,7 +28,7 @@ __device__ __forceinline__ ArtI<T> rigid_inertia(const Link<T> &L) {
 
 // E S E^T for symmetric S
 template <typename T>
-__device__ __forceinline__ S3<T> rot_sym(const M3<T> &E, const S3<T> &S) {
+RB_HD S3<T> rot_sym(const M3<T> &E, const S3<T> &S) {
     const T s[9] = {S.xx, S.xy, S.xz, S.xy, S.yy, S.yz, S.xz, S.yz, S.zz};
     T t[9];
 #pragma unroll
@@ -44,7 +44,7 @@ __device__ __forceinline__ S3<T> rot_sym(const M3<T> &E, const S3<T> &S) {
 
 // E B E^T for general B
 template <typename T>
-__device__ __forceinline__ M3<T> rot_full(const M3<T> &E, const M3<T> &Bm) {
+RB_HD M3<T> rot_full(const M3<T> &E, const M3<T> &Bm) {
     T t[9];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
@@ -63,7 +63,7 @@ __device__ __forceinline__ M3<T> rot_full(const M3<T> &E, const M3<T> &Bm) {
 // X^T Ia X for the child->parent transform (E, p): rotate blocks, then shift by
 // P = [p]x:  B'' = B' + P M',  A'' = A' + P B'^T + B'' P^T,  M'' = M'.
 template <typename T>
-__device__ __forceinline__ ArtI<T> to_parent(const M3<T> &E, const V3<T> &p, const ArtI<T> &I) {
+RB_HD ArtI<T> to_parent(const M3<T> &E, const V3<T> &p, const ArtI<T> &I) {
     const S3<T> A1 = rot_sym(E, I.A);
     const M3<T> B1 = rot_full(E, I.B);
     const S3<T> M1 = rot_sym(E, I.M);
@@ -104,7 +104,7 @@ __device__ __forceinline__ ArtI<T> to_parent(const M3<T> &E, const V3<T> &p, con
 #define RB_SPLIT_ROT 0
 #endif
 template <typename T>
-__device__ __forceinline__ S3<T> rot_sym_z(T c, T s, T C, T S2, const S3<T> &S) {
+RB_HD S3<T> rot_sym_z(T c, T s, T C, T S2, const S3<T> &S) {
     const T h = T(0.5) * (S.xx + S.yy), g = T(0.5) * (S.xx - S.yy);
     return S3<T>{fmadd(g, C, fmadd(-S.xy, S2, h)), fmadd(g, S2, S.xy * C), fmadd(c, S.xz, -s * S.yz),
                  fmadd(-g, C, fmadd(S.xy, S2, h)), fmadd(s, S.xz, c * S.yz), S.zz};
@@ -112,7 +112,7 @@ __device__ __forceinline__ S3<T> rot_sym_z(T c, T s, T C, T S2, const S3<T> &S) 
 
 // to_parent with the symmetric blocks rotated as R_p (Rz S Rz^T) R_p^T.
 template <typename T>
-__device__ __forceinline__ ArtI<T> to_parent_split(const M3<T> &Rp, T c, T s, const M3<T> &E, const V3<T> &p,
+RB_HD ArtI<T> to_parent_split(const M3<T> &Rp, T c, T s, const M3<T> &E, const V3<T> &p,
                                                    const ArtI<T> &I) {
     const T C = fmadd(c, c, -s * s), S2 = (c + c) * s;
     ArtI<T> J = I;
@@ -147,7 +147,7 @@ __device__ __forceinline__ ArtI<T> to_parent_split(const M3<T> &Rp, T c, T s, co
 }
 
 template <typename T>
-__device__ __forceinline__ void add_rigid(ArtI<T> &I, const Link<T> &L) {
+RB_HD void add_rigid(ArtI<T> &I, const Link<T> &L) {
     I.A.xx += L.Io.xx; I.A.xy += L.Io.xy; I.A.xz += L.Io.xz;
     I.A.yy += L.Io.yy; I.A.yz += L.Io.yz; I.A.zz += L.Io.zz;
     I.B.m[1] -= L.h.z; I.B.m[2] += L.h.y;

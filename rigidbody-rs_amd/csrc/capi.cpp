@@ -2,8 +2,11 @@
 //
 // Drop-in for the Rust cdylib rigidbody_bindings (rigidbody_bindings/src/lib.rs:8-78):
 // same six symbols and result layouts, plus batched device-pointer entry points.
-// Every compute entry point runs a HIP kernel on the current device; there is no CPU
-// compute path in this library (model loading and argument checks only).
+// Every batched entry point runs a HIP kernel on the current device (no CPU fallback).  The
+// reference's single-configuration queries run on the calling host thread with the same
+// lane bodies compiled for the host (host_eval.cpp: SURVEY §8(d) config 1 is a CPU path, and
+// a GPU round trip costs ~25x the recursion), unless the model needs hipRTC (trees) or the
+// caller asks for the GPU (tuning single_gpu).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -23,6 +26,7 @@
 #include "model.hpp"
 #include "tuning.hpp"
 #include "jit.hpp"
+#include "host_eval.hpp"
 
 #include "fr3_embedded.inc"  // kFr3Urdf: compact FR3 description (tools/gen_fixtures.py)
 
@@ -143,12 +147,6 @@ int device_consts(const Multibody *mb, const T **out) {
     return RB_OK;
 }
 
-// Resident grid-stride form of a JIT kernel (tuning.hpp policies).
-bool jit_stream(rbamd::JitKind kind, bool f64, int n) {
-    return (kind == rbamd::JitKind::Rnea && rbamd::rnea_use_stream(f64, n, true)) ||
-           (kind == rbamd::JitKind::Fd && rbamd::tuning().fd_stream > 0);
-}
-
 // The hipRTC kernel of `kind` for this model on the current device, or nullptr (the
 // precompiled generic kernel then runs).
 // pack: configurations per lane, 0 = the jit_pack policy (jit.cpp).
@@ -156,16 +154,15 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     if (!rbamd::jit_enabled()) return nullptr;
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
-    const bool stream = jit_stream(kind, f64, mb->model.n);
     const bool fst = fast && !f64;
-    if (pack <= 0) pack = rbamd::jit_pack(kind, f64, mb->model.n, stream);
+    if (pack <= 0) pack = rbamd::jit_pack(kind, f64, mb->model.n);
     const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
-                            (fst ? ":fast" : ":precise") + (stream ? ":stream" : ":lane") +
-                            rbamd::jit_tag(kind, f64, mb->model.n) + ":q" + std::to_string(pack);
+                            (fst ? ":fast" : ":precise") + rbamd::jit_tag(kind, f64, mb->model.n) + ":q" +
+                            std::to_string(pack);
     std::lock_guard<std::mutex> lk(mb->mu);
     auto it = mb->jit.find(key);
     if (it == mb->jit.end()) {
-        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, stream, pack)).first;
+        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, pack)).first;
         mb->jit_device[key] = d;
     }
     return it->second.function ? &it->second : nullptr;
@@ -194,34 +191,23 @@ hipError_t no_generic(const Multibody *mb) {
 // of it (2 blocks of 512 configurations per CU x 256 CUs) -- 2^18.
 constexpr uint32_t kPackMinBatch = 1u << 18;
 
-hipError_t jit_launch(const rbamd::JitKernel *jk, hipFunction_t fn, uint32_t B, void **args, hipStream_t s) {
-    const unsigned per_block = 256u * (unsigned)jk->pack * (unsigned)jk->tiles;
-    const unsigned full = (unsigned)(((uint64_t)B + per_block - 1) / per_block);
-    unsigned g = full;
-    if (jk->stream) {
-        const int f = rbamd::tuning().grid_factor < 1 ? 1 : rbamd::tuning().grid_factor;
-        g = jk->resident * (unsigned)f < full ? jk->resident * (unsigned)f : full;
-    }
-    return hipModuleLaunchKernel(fn, g, 1, 1, 256u * (unsigned)jk->tiles, 1, 1, 0, s, args, nullptr);
+hipError_t jit_launch(const rbamd::JitKernel *jk, uint32_t B, void **args, hipStream_t s) {
+    const unsigned per_block = 256u * (unsigned)jk->pack;
+    const unsigned g = (unsigned)(((uint64_t)B + per_block - 1) / per_block);
+    return hipModuleLaunchKernel(jk->function, g, 1, 1, 256u, 1, 1, 0, s, args, nullptr);
 }
 
 // tiled: the [ceil(B/256)][n][256] layout (kernels.hpp); the JIT lane kernels and the
-// generic lane kernels take it through their block stride; the SoA-only forms (JIT
-// grid-stride / LDS-tiled RNEA) are never chosen for it.
+// generic lane kernels take it through their block stride (the generic grid-stride RNEA is
+// SoA-only and never chosen for it).
 template <typename T>
 hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *qdd, T *tau,
                            uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig());
-    if (jk && !(tiled && jk->stream)) {
+    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig())) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&lda, (void *)&bs};
-        hipFunction_t fn = jk->function;
-        const auto a16 = [](const void *p) { return ((uintptr_t)p & 15u) == 0; };
-        if (!tiled && jk->tile_function && rbamd::tuning().rnea_tile && a16(q) && a16(qd) && a16(qdd) && a16(tau) &&
-            ((uint64_t)ld * sizeof(T)) % 16 == 0)
-            fn = jk->tile_function;
-        return jit_launch(jk, fn, B, args, s);
+        return jit_launch(jk, B, args, s);
     }
     if (!mb->model.serial_revolute()) return no_generic(mb);
     return rbamd::launch_rnea<T>(mb->model.n, mdl, q, qd, qdd, tau, B, ld, s, fast_trig(), tiled);
@@ -237,7 +223,7 @@ hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T 
     if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Fd, sizeof(T) == 8, fast_trig(), pack)) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau, (void *)&qdd, (void *)&B, (void *)&lda, (void *)&bs};
-        return jit_launch(jk, jk->function, B, args, s);
+        return jit_launch(jk, B, args, s);
     }
     if (!mb->model.serial_revolute()) return no_generic(mb);
     return rbamd::launch_aba<T>(mb->model.n, mdl, q, qd, tau, qdd, B, ld, s, fast_trig(), tiled);
@@ -250,7 +236,7 @@ hipError_t launch_rollout_any(const Multibody *mb, const T *mdl, T *q, T *qd, co
     if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Rollout, sizeof(T) == 8, fast_trig())) {
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau_seq, (void *)&dt, (void *)&K, (void *)&traj,
                         (void *)&B, (void *)&ld};
-        return jit_launch(jk, jk->function, B, args, s);
+        return jit_launch(jk, B, args, s);
     }
     if (!mb->model.serial_revolute()) return no_generic(mb);
     return rbamd::launch_rollout<T>(mb->model.n, mdl, q, qd, tau_seq, dt, K, traj, B, ld, s, fast_trig());
@@ -262,7 +248,7 @@ hipError_t launch_crba_any(const Multibody *mb, const T *mdl, const T *q, T *H, 
     if (B == 0) return hipSuccess;
     if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Crba, sizeof(T) == 8, false)) {
         void *args[] = {(void *)&q, (void *)&H, (void *)&B, (void *)&ld};
-        return jit_launch(jk, jk->function, B, args, s);
+        return jit_launch(jk, B, args, s);
     }
     if (!mb->model.serial_revolute()) return no_generic(mb);
     return rbamd::launch_crba<T>(mb->model.n, mdl, q, H, B, ld, s);
@@ -279,7 +265,7 @@ hipError_t launch_kin_any(const Multibody *mb, bool jac, const double *mdl, cons
     const rbamd::JitKernel *jk = jit_get(mb, jac ? rbamd::JitKind::Jac : rbamd::JitKind::FwdKin, true, false);
     if (!jk) return no_generic(mb);
     void *args[] = {(void *)&q, (void *)&out, (void *)&B, (void *)&ld};
-    return jit_launch(jk, jk->function, B, args, s);
+    return jit_launch(jk, B, args, s);
 }
 
 constexpr int64_t kChunk = int64_t(1) << 28;  // per-launch batch cap: b * sizeof(T) < 2^32
@@ -329,6 +315,22 @@ int staging(size_t doubles, Staging **out) {
     }
     *out = &s;
     return RB_OK;
+}
+
+// Host evaluation of one single-configuration query (host_eval.cpp) when the model and CPU
+// allow it and the caller has not asked for the GPU (tuning single_gpu); `eval(out)` fills
+// the result.  Returns the malloc'd result, or nullptr with *used = false to take the GPU.
+template <typename F>
+double *single_host(const Multibody *mb, const double *const *inputs, int nin, size_t nout, bool *used, F eval) {
+    *used = false;
+    if (!mb || rbamd::tuning().single_gpu != 0 || !rbamd::host_eval_supported(mb->model)) return nullptr;
+    for (int k = 0; k < nin; ++k)
+        if (!inputs[k]) { set_err(RB_ERR_NULL, "NULL input vector"); *used = true; return nullptr; }
+    *used = true;
+    double *res = static_cast<double *>(std::malloc(nout * sizeof(double)));
+    if (!res) { set_err(RB_ERR_ARG, "out of host memory"); return nullptr; }
+    if (!eval(res)) { std::free(res); *used = false; return nullptr; }
+    return res;
 }
 
 // Runs one single-configuration query on the GPU: `nin` input vectors of n doubles,
@@ -479,8 +481,9 @@ template <typename T>
 int fill_uniform(T *x, int rows, int64_t batch, int64_t ld, const double *lo, const double *hi, uint64_t seed,
                  void *stream) {
     if (!x || !lo || !hi) return set_err(RB_ERR_NULL, "NULL argument");
-    if (rows < 1 || batch < 0 || ld < batch || batch >= (int64_t(1) << 40))
-        return set_err(RB_ERR_ARG, "bad fill shape");
+    if (rows < 1 || batch < 0 || ld < batch) return set_err(RB_ERR_ARG, "bad fill shape");
+    // one launch; the generator's lane index is 32-bit (b * sizeof(T) < 2^32 as the dynamics)
+    if (batch > kChunk) return set_err(RB_ERR_ARG, "fill batch above 2^28 configurations not supported");
     if (batch == 0) return RB_OK;
     hipStream_t s = (hipStream_t)stream;
     std::vector<double> lohi(2 * (size_t)rows);
@@ -494,13 +497,8 @@ int fill_uniform(T *x, int rows, int64_t batch, int64_t ld, const double *lo, co
     e = hipMemcpyAsync(d, lohi.data(), lohi.size() * sizeof(double), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_err(e, "hipMemcpyAsync");
     int rc = RB_OK;
-    for (int64_t b0 = 0; b0 < batch && rc == RB_OK; b0 += kChunk) {
-        const int64_t nb = batch - b0 < kChunk ? batch - b0 : kChunk;
-        // the generator indexes by the absolute configuration index b0 + b
-        e = rbamd::launch_fill_uniform<T>(x + b0, rows, (uint32_t)nb, ld, d, seed, s);
-        if (e != hipSuccess) rc = hip_err(e, "fill launch");
-        if (b0 + kChunk < batch) { rc = set_err(RB_ERR_ARG, "fill batch above 2^30 not supported"); }
-    }
+    e = rbamd::launch_fill_uniform<T>(x, rows, (uint32_t)batch, ld, d, seed, s);
+    if (e != hipSuccess) rc = hip_err(e, "fill launch");
     (void)hipFreeAsync(d, s);
     // the host-side lohi vector dies here; make sure the copy has consumed it
     e = hipStreamSynchronize(s);
@@ -540,6 +538,11 @@ void multibody_free(Multibody *mb) {
 double *multibody_rnea(const Multibody *mb, const double *q, const double *dq, const double *ddq) {
     const double *in[3] = {q, dq, ddq};
     const size_t n = mb ? (size_t)mb->model.n : 0;
+    bool host = false;
+    double *r = single_host(mb, in, 3, n, &host, [&](double *o) {
+        return rbamd::host_rnea(mb->model, mb->pk64.data(), q, dq, ddq, o);
+    });
+    if (host) return r;
     return single_query(mb, in, 3, n, [&](double *din, double *dout, hipStream_t s) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
@@ -552,6 +555,11 @@ double *multibody_rnea(const Multibody *mb, const double *q, const double *dq, c
 double *multibody_crba(const Multibody *mb, const double *q) {
     const double *in[1] = {q};
     const size_t n = mb ? (size_t)mb->model.n : 0;
+    bool host = false;
+    double *r = single_host(mb, in, 1, n * n, &host, [&](double *o) {
+        return rbamd::host_crba(mb->model, mb->pk64.data(), q, o);
+    });
+    if (host) return r;
     return single_query(mb, in, 1, n * n, [&](double *din, double *dout, hipStream_t s) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
@@ -564,6 +572,11 @@ double *multibody_crba(const Multibody *mb, const double *q) {
 double *multibody_fwd_kin(const Multibody *mb, const double *q) {
     const double *in[1] = {q};
     const size_t n = mb ? (size_t)mb->model.n : 0;
+    bool host = false;
+    double *r = single_host(mb, in, 1, 3, &host, [&](double *o) {
+        return rbamd::host_fwd_kin(mb->model, mb->pk64.data(), q, o);
+    });
+    if (host) return r;
     return single_query(mb, in, 1, 3, [&](double *din, double *dout, hipStream_t s) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
@@ -576,6 +589,11 @@ double *multibody_fwd_kin(const Multibody *mb, const double *q) {
 double *multibody_jac(const Multibody *mb, const double *q) {
     const double *in[1] = {q};
     const size_t n = mb ? (size_t)mb->model.n : 0;
+    bool host = false;
+    double *r = single_host(mb, in, 1, 6 * n, &host, [&](double *o) {
+        return rbamd::host_jac(mb->model, mb->pk64.data(), q, o);
+    });
+    if (host) return r;
     return single_query(mb, in, 1, 6 * n, [&](double *din, double *dout, hipStream_t s) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
@@ -679,12 +697,16 @@ int multibody_kernel_path(const Multibody *mb, int kind, int f64) {
 
 int multibody_rnea_kernel_path(const Multibody *mb, int f64) { return multibody_kernel_path(mb, 0, f64); }
 
+int multibody_single_config_path(const Multibody *mb) {
+    if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
+    return (rbamd::tuning().single_gpu == 0 && rbamd::host_eval_supported(mb->model)) ? 0 : 1;
+}
+
 int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
     if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
     const std::string src = rbamd::jit_source(mb->model, (rbamd::JitKind)kind, f64 != 0,
-                                              kind != 2 && kind < 4 && fast_trig() && !f64,
-                                              jit_stream((rbamd::JitKind)kind, f64 != 0, mb->model.n));
+                                              kind != 2 && kind < 4 && fast_trig() && !f64);
     if (buf && cap > 0) {
         const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
         std::memcpy(buf, src.data(), n);
@@ -699,7 +721,6 @@ int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char
     std::vector<char> code;
     std::string err;
     if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && kind < 4 && fast_trig() && !f64,
-                            jit_stream((rbamd::JitKind)kind, f64 != 0, mb->model.n),
                             arch ? arch : "gfx950", &code, &err))
         return -set_err(RB_ERR_HIP, err);
     return (int64_t)code.size();
@@ -761,25 +782,11 @@ int rb_from_tiled_f64(const double *src, double *dst, int64_t ld, int rows, int6
 
 int rb_set_tuning(const char *key, int value) {
     if (!key) return set_err(RB_ERR_NULL, "NULL key");
-    rbamd::Tuning &t = rbamd::tuning();
-    const std::string k(key);
-    if (k == "rnea_stream") t.rnea_stream = value;
-    else if (k == "grid_factor") t.grid_factor = value;
-    else if (k == "jit") t.jit = value;
-    else if (k == "rnea_tile") t.rnea_tile = value;
-    else if (k == "rnea_nt") t.rnea_nt = value;
-    else if (k == "fd_nt") t.fd_nt = value;
-    else if (k == "jit_waves") t.jit_waves = value;
-    else if (k == "jit_variant") t.jit_variant = value;
-    else if (k == "opaque_consts") t.opaque_consts = value;
-    else if (k == "fd_stream") t.fd_stream = value;
-    else if (k == "pack") t.pack = value;
-    else if (k == "f64_tab") t.f64_tab = value;
-    else if (k == "rnea_seg") t.rnea_seg = value;
-    else if (k == "rnea_tiles") t.rnea_tiles = value;
-    else if (k == "split_rot") t.split_rot = value;
-    else return set_err(RB_ERR_ARG, "unknown tuning key: " + k);
-    return RB_OK;
+    switch (rbamd::tuning_set(key, value)) {
+        case 0: return RB_OK;
+        case 2: return set_err(RB_ERR_ARG, std::string("experimental tuning key (set RB_EXPERIMENTAL=1): ") + key);
+        default: return set_err(RB_ERR_ARG, std::string("unknown tuning key: ") + key);
+    }
 }
 
 // ------------------------------------------------------------- batched (device)

@@ -10,7 +10,7 @@ namespace rbamd {
 namespace dev {
 
 template <typename T, int N, bool FAST, typename Out>
-__device__ __forceinline__ void crba_eval(const T *mdl, const T (&qv)[N], Out &&out) {
+RB_HD void crba_eval(const T *mdl, const T (&qv)[N], Out &&out) {
     T cs[N], sn[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);

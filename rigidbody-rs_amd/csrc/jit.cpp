@@ -17,8 +17,6 @@ namespace rbamd {
 
 bool jit_enabled() { return tuning().jit != 0; }
 
-bool jit_tile_ok(int n, bool f64) { return 3 * n * 256 * (f64 ? 8 : 4) <= 48 * 1024; }
-
 namespace {
 
 double snap(double x) {
@@ -62,43 +60,29 @@ int jit_waves(JitKind kind, bool f64, int n) {
     return (kind == JitKind::Rollout && !f64 && n <= 8) ? 4 : 0;
 }
 
-int jit_pack(JitKind kind, bool f64, int n, bool stream) {
-    // The rollout is not paired: with its K loop around the dynamics the pair needs 256 VGPRs
-    // (1 wave/SIMD) unpinned, or spills at 2-4 waves with pinned constants.
-    if (f64 || stream || (kind != JitKind::Rnea && kind != JitKind::Fd)) return 1;
+int jit_pack(JitKind kind, bool f64, int n) {
+    // Only fp32 forward dynamics pairs.  The rollout is not paired: with its K loop around the
+    // dynamics the pair needs 256 VGPRs (1 wave/SIMD) unpinned, or spills at 2-4 waves with
+    // pinned constants.  The RNEA pair (128 VGPRs, 4 waves/SIMD instead of 8) measured slower,
+    // 22.6 vs 21.0 us, although it issues half the VALU work, and was removed.
+    if (f64 || kind != JitKind::Fd) return 1;
     const int v = tuning().pack;
     if (v >= 0) return v >= 2 ? 2 : 1;
-    // Auto: forward dynamics of chains up to 8 links (FR3 fp32 2^20 tiled: 28.7 vs 30.7 us;
-    // 200 VGPRs for the pair, 2 waves/SIMD).  RNEA stays one per lane: its pair needs 128
-    // VGPRs (4 waves/SIMD instead of 8) and measured slower, 22.6 vs 21.0 us, although it
-    // issues half the VALU work.  The 30-link chain needs ~240 VGPRs for one configuration.
-    return (kind == JitKind::Fd && n <= 8) ? 2 : 1;
-}
-
-int jit_tiles(JitKind kind, int pack, bool stream) {
-    if (kind != JitKind::Rnea || pack != 1 || stream) return 1;
-    const int v = tuning().rnea_tiles;
-    return v >= 4 ? 4 : (v >= 2 ? 2 : 1);
+    // Auto: chains up to 8 links (FR3 fp32 2^20 tiled: 28.7 vs 30.7 us; 200 VGPRs for the
+    // pair, 2 waves/SIMD).  The 30-link chain needs ~240 VGPRs for one configuration.
+    return n <= 8 ? 2 : 1;
 }
 
 bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
 
-// Segments of the RNEA lane kernel (rnea_eval_seg) for a serial chain of n links; 1 = one pass.
-int jit_rnea_seg(const Model &m, bool f64) {
-    (void)f64;
-    if (!m.serial_revolute()) return 1;
-    const int v = tuning().rnea_seg;
-    if (v >= 0) return v < 1 ? 1 : (v > m.n ? m.n : v);
-    return 1;
-}
-
 std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
-           std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n, false)) +
-           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":s" + std::to_string(tuning().rnea_seg) + ":b" + std::to_string(tuning().rnea_tiles) + ":r" + std::to_string(tuning().split_rot) + ":v" + std::to_string(tuning().jit_variant);
+           std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n)) +
+           ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":r" + std::to_string(tuning().split_rot) + ":v" +
+           std::to_string(tuning().jit_variant);
 }
 
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack_req) {
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req) {
     std::vector<double> pk = m.pack_f64();
     for (int i = 0; i < m.n; ++i) {
         double *c = &pk[(size_t)i * kLinkStride];
@@ -106,7 +90,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         for (int k = 0; k < 3; ++k) c[kP + k] = snap(c[kP + k]);
     }
     const char *F = fast ? "true" : "false";
-    const int pack = pack_req > 0 ? pack_req : jit_pack(kind, f64, m.n, stream);
+    const int pack = pack_req > 0 ? pack_req : jit_pack(kind, f64, m.n);
     std::ostringstream o;
     o << "#define RB_NT " << jit_nt(kind) << "\n";
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
@@ -173,8 +157,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
         "  if (bA >= B) return;\n"
         "  const int64_t oA = (int64_t)(2u * blockIdx.x) * bs;\n"
         "  const int64_t oB = bA + 256u < B ? oA + bs : oA;\n";
-    const int tiles = jit_tiles(kind, pack, stream);
-    std::string head_s = "extern \"C\" __global__ __launch_bounds__(" + std::to_string(256 * tiles) + ") ";
+    std::string head_s = "extern \"C\" __global__ __launch_bounds__(256) ";
     if (const int w = jit_waves(kind, f64, m.n))
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
     head_s += "void ";
@@ -184,46 +167,10 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     if (kind == JitKind::Rnea) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
-        if (pack == 2) {
-            o << pair_prologue;
-            o << "  rbamd::dev::rnea_lane2<N, " << F
-              << ", Topo>(kModel, q, qd, qdd, tau, oA, oB, threadIdx.x * 4u, ld);\n";
-        } else if (stream) {  // SoA only (capi.cpp)
-            o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
-            o << "  if (b >= B) return;\n";
-            o << "  T qv[N], qdv[N], qddv[N];\n";
-            o << "  rbamd::dev::load_cfg<T, N>(q, qd, qdd, ld, b * (uint32_t)sizeof(T), qv, qdv, qddv);\n";
-            o << "  rbamd::dev::rnea_stream_lane<T, N, " << F
-              << ", Topo>(kModel, q, qd, qdd, tau, b, gridDim.x * 256u, B, ld, qv, qdv, qddv);\n";
-        } else {
-            // tile k = blockIdx.x * tiles + threadIdx.x / 256 (wave-uniform: readfirstlane keeps
-            // the row bases in SGPRs, the saddr form), lane threadIdx.x % 256
-            if (tiles == 1)
-                o << "  const uint32_t tl = blockIdx.x, lane = threadIdx.x;\n";
-            else
-                o << "  const uint32_t tl = blockIdx.x * " << tiles
-                  << "u + __builtin_amdgcn_readfirstlane(threadIdx.x >> 8), lane = threadIdx.x & 255u;\n";
-            o << "  if (tl * 256u + lane >= B) return;\n";
-            o << "  const int64_t o = (int64_t)tl * bs;\n";
-            if (const int S = jit_rnea_seg(m, f64); S > 1)
-                o << "  rbamd::dev::rnea_lane_seg<T, N, " << S << ", " << F
-                  << ">(kModel, q + o, qd + o, qdd + o, tau + o, lane, ld);\n";
-            else
-                o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, lane, ld);\n";
-        }
-        o << "}\n";
-        if (pack == 1 && tiles == 1 && jit_tile_ok(m.n, f64)) {  // SoA only
-            o << head << "rb_jit_tile(const T *__restrict__ q, const T *__restrict__ qd, "
-                 "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
-            o << "  __shared__ T tile[3 * N * 256];\n";
-            o << "  const uint32_t b0 = blockIdx.x * 256u;\n";
-            o << "  if (b0 + 256u <= B) {\n";
-            o << "    rbamd::dev::rnea_tile<T, N, " << F << ", Topo>(kModel, q, qd, qdd, tau, b0, ld, tile);\n";
-            o << "  } else {\n";
-            o << "    const uint32_t b = b0 + threadIdx.x;\n";
-            o << "    if (b < B) rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q, qd, qdd, tau, b, ld);\n";
-            o << "  }\n}\n";
-        }
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+        o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n}\n";
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
@@ -231,8 +178,6 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
             o << pair_prologue;
             o << "  rbamd::dev::aba_lane2<N, " << F
               << ", Topo>(kModel, q, qd, tau, qdd, oA, oB, threadIdx.x * 4u, ld);\n}\n";
-        } else if (stream) {
-            o << "  rbamd::dev::aba_stream<T, N, " << F << ", Topo>(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
         } else {
             o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
             o << "  if (b >= B) return;\n";
@@ -260,19 +205,16 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool s
     }
     std::string src = o.str();
     if (tab) {  // every kernel fills the block's sincos table first (all lanes still present)
-        for (const char *name : {"rb_jit_kernel(", "rb_jit_tile("}) {
-            const size_t at = src.find(name);
-            if (at == std::string::npos) continue;
-            const size_t body = src.find(") {\n", at);
-            if (body != std::string::npos) src.insert(body + 4, "  rbamd::dev::sctab_init();\n");
-        }
+        const size_t at = src.find("rb_jit_kernel(");
+        const size_t body = at == std::string::npos ? at : src.find(") {\n", at);
+        if (body != std::string::npos) src.insert(body + 4, "  rbamd::dev::sctab_init();\n");
     }
     return src;
 }
 
-bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream, const std::string &arch,
+bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
                  std::vector<char> *code, std::string *error, int pack) {
-    const std::string src = jit_source(m, kind, f64, fast, stream, pack);
+    const std::string src = jit_source(m, kind, f64, fast, pack);
     hiprtcProgram prog = nullptr;
     if (hiprtcCreateProgram(&prog, src.c_str(), "rb_jit.hip", kJitHeaderCount, kJitHeaderSources,
                             kJitHeaderNames) != HIPRTC_SUCCESS) {
@@ -299,11 +241,9 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream,
     return true;
 }
 
-JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack) {
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack) {
     JitKernel jk;
-    jk.stream = stream;
-    jk.pack = pack > 0 ? pack : jit_pack(kind, f64, m.n, stream);
-    jk.tiles = jit_tiles(kind, jk.pack, stream);
+    jk.pack = pack > 0 ? pack : jit_pack(kind, f64, m.n);
     int dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
@@ -311,16 +251,13 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stre
         return jk;
     }
     std::vector<char> code;
-    if (!jit_compile(m, kind, f64, fast, stream, prop.gcnArchName, &code, &jk.error, jk.pack)) return jk;
+    if (!jit_compile(m, kind, f64, fast, prop.gcnArchName, &code, &jk.error, jk.pack)) return jk;
     hipError_t e = hipModuleLoadData(&jk.module, code.data());
     if (e != hipSuccess) {
         jk.error = std::string("hipModuleLoadData: ") + hipGetErrorString(e);
         jk.module = nullptr;
         return jk;
     }
-    if (kind == JitKind::Rnea && jk.pack == 1 && jk.tiles == 1 && jit_tile_ok(m.n, f64) &&
-        hipModuleGetFunction(&jk.tile_function, jk.module, "rb_jit_tile") != hipSuccess)
-        jk.tile_function = nullptr;
     e = hipModuleGetFunction(&jk.function, jk.module, "rb_jit_kernel");
     if (e != hipSuccess) {
         jk.error = std::string("hipModuleGetFunction: ") + hipGetErrorString(e);
@@ -328,13 +265,6 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stre
         jk.module = nullptr;
         jk.function = nullptr;
         return jk;
-    }
-    if (stream) {
-        int per_cu = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jk.function, 256, 0) != hipSuccess ||
-            per_cu < 1)
-            per_cu = 1;
-        jk.resident = (unsigned)per_cu * (unsigned)prop.multiProcessorCount;
     }
     return jk;
 }

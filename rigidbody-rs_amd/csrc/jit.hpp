@@ -29,23 +29,16 @@ enum class JitKind : int { Rnea = 0, Fd = 1, Crba = 2, Rollout = 3, FwdKin = 4, 
 
 struct JitKernel {
     hipModule_t module = nullptr;
-    hipFunction_t function = nullptr;       // one configuration per lane (any layout)
-    hipFunction_t tile_function = nullptr;  // LDS-tiled, 16-byte global accesses (aligned SoA)
-    bool stream = false;        // grid-stride form: launch a resident-sized grid
-    int pack = 1;               // configurations per lane (2: paired fp32 lanes, 512 per block)
-    int tiles = 1;              // 256-configuration tiles per workgroup (256 x tiles threads)
-    unsigned resident = 0;      // resident blocks (occupancy x CUs) for the stream form
-    std::string error;          // non-empty when compilation failed
+    hipFunction_t function = nullptr;  // the lane kernel (any layout)
+    int pack = 1;                      // configurations per lane (2: paired fp32 lanes, 512 per block)
+    std::string error;                 // non-empty when compilation failed
 };
 
 bool jit_enabled();
 
-// The LDS-tiled kernel form is generated when the 3N-row input tile fits in 48 KiB.
-bool jit_tile_ok(int n, bool f64);
-
 // Generated HIP source for one specialised kernel (exposed for tests / inspection).
 // pack: configurations per lane, 0 = the jit_pack policy.
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack = 0);
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0);
 
 // Non-temporal access bits of `kind`'s JIT source, and the cache-key suffix of every
 // tuning value that changes the source (tuning.hpp).
@@ -53,16 +46,14 @@ int jit_nt(JitKind kind);
 bool jit_opaque(JitKind kind, bool f64, int n);
 int jit_waves(JitKind kind, bool f64, int n);
 // Configurations per lane of `kind`'s lane kernel (tuning `pack`): 2 = paired fp32 lanes.
-int jit_pack(JitKind kind, bool f64, int n, bool stream);
-// 256-configuration tiles per workgroup of `kind`'s lane kernel (tuning rnea_tiles).
-int jit_tiles(JitKind kind, int pack, bool stream);
+int jit_pack(JitKind kind, bool f64, int n);
 std::string jit_tag(JitKind kind, bool f64, int n);
 
 // hipRTC compilation only (no device needed): fills `code` with the code object.
-bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, bool stream, const std::string &arch,
+bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
                  std::vector<char> *code, std::string *error, int pack = 0);
 
 // Compiles and loads the kernel on the current device.  Never throws.
-JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, bool stream, int pack = 0);
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0);
 
 }  // namespace rbamd

@@ -64,7 +64,7 @@ hipError_t rnea_go(const T *mdl, const T *q, const T *qd, const T *qdd, T *tau, 
                    hipStream_t s, bool tiled) {
     const Tuning &tn = tuning();
     const unsigned full = dev::grid_for(B);
-    if (!tiled && rnea_use_stream(sizeof(T) == 8, N, false)) {
+    if (!tiled && rnea_use_stream(sizeof(T) == 8, N)) {
         auto kfn = dev::rnea_stream_kernel<T, N, F>;
         const unsigned g = stream_grid((const void *)kfn, dev::kBlock, full, tn.grid_factor);
         hipLaunchKernelGGL(kfn, dim3(g), dim3(dev::kBlock), 0, s, mdl, q, qd, qdd, tau, B, ld);

@@ -9,8 +9,7 @@ namespace rbamd {
 namespace dev {
 
 // ----------------------------------------------------------------------------- RNEA
-// Per-link steps of the serial-chain RNEA, shared by the one-pass form (rnea_eval) and the
-// segmented form (rnea_eval_seg) so both run the identical operation sequence.
+// Per-link steps of the serial-chain RNEA (rnea_eval).
 template <typename T>
 struct RneaState {
     V3<T> w, v, aw, av;  // link velocity / acceleration (rot, lin), link coordinates
@@ -18,7 +17,7 @@ struct RneaState {
 
 // Link 0: v_{-1} = 0, a_{-1} = (0, (0,0,+g)) -- multibody.rs:116-120
 template <typename T, bool FAST>
-__device__ __forceinline__ void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn, T &cs,
+RB_HD void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn, T &cs,
                                           V3<T> &fn, V3<T> &ff) {
     const Link<T> L = load_link(mdl, 0);
     sin_cos<FAST>(q0, sn, cs);
@@ -39,7 +38,7 @@ __device__ __forceinline__ void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, Rne
 
 // Link j >= 1: forward sweep step (multibody.rs:122-141).
 template <typename T, bool FAST>
-__device__ __forceinline__ void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, T &sn, T &cs,
+RB_HD void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, T &sn, T &cs,
                                          V3<T> &fn, V3<T> &ff) {
     const Link<T> L = load_link(mdl, j);
     sin_cos<FAST>(qj, sn, cs);
@@ -66,7 +65,7 @@ __device__ __forceinline__ void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qdd
 
 // Backward sweep step: f_{j-1} += X_j^-1 f_j  (multibody.rs:145-150).
 template <typename T>
-__device__ __forceinline__ void rnea_bwd(const T *mdl, int j, T cj, T sj, const V3<T> &ffj, const V3<T> &fnj,
+RB_HD void rnea_bwd(const T *mdl, int j, T cj, T sj, const V3<T> &ffj, const V3<T> &fnj,
                                          V3<T> &ffp, V3<T> &fnp) {
     const T *c = mdl + j * kLinkStride;
     const M3<T> Rp{{c[kE0 + 0], c[kE0 + 1], c[kE0 + 2], c[kE0 + 3], c[kE0 + 4], c[kE0 + 5],
@@ -84,7 +83,7 @@ __device__ __forceinline__ void rnea_bwd(const T *mdl, int j, T cj, T sj, const 
 // per-link forces never leave registers.  One call evaluates the configuration whose
 // joint values are in (qv, qdv, qddv) and hands tau_j to `out(j, value)`.
 template <typename T, int N, bool FAST, typename Out>
-__device__ __forceinline__ void rnea_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
+RB_HD void rnea_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
                                           const T (&qddv)[N], Out &&out) {
     T cs[N], sn[N];
     V3<T> fn[N], ff[N];  // per-link spatial force: moment n (rot), force f (lin)
@@ -103,61 +102,8 @@ __device__ __forceinline__ void rnea_eval(const T *mdl, const T (&qv)[N], const 
     out(0, fn[0].z);
 }
 
-// Segmented form for long chains: the per-link state the backward sweep needs (force 6,
-// cos/sin 2 -- 8 values per link, 240 VGPRs for 30 links, 2 waves/SIMD) is held for one
-// segment of ceil(N/S) links at a time.  Segments are processed top (leaf) first: each pass
-// reloads the inputs of links 0..hi-1 (`load(j, q, qd, qdd)`; L2/MALL-resident after the
-// first pass), recomputes the forward sweep up to its top link keeping only its own links'
-// state, and runs its part of the backward sweep; the force of its lowest link is carried
-// (with that link's cos/sin) into the next pass, where the same rnea_bwd step applies it --
-// so every tau is computed by exactly the operations of rnea_eval (bit-identical), at
-// (S+1)/2 times the forward-sweep work.
-template <typename T, int N, int S, bool FAST, typename Load, typename Out>
-__device__ __forceinline__ void rnea_eval_seg(const T *mdl, Load &&load, Out &&out) {
-    constexpr int L = (N + S - 1) / S;
-    T ccs = T(0), csn = T(0);
-    V3<T> cff = v3(T(0), T(0), T(0)), cfn = cff;
-    cfor_rev<S>([&](auto sc) {
-        constexpr int seg = decltype(sc)::value;
-        constexpr int lo = seg * L, hi = (lo + L < N) ? lo + L : N;
-        if constexpr (lo < N) {
-            T qv[hi], qdv[hi], qddv[hi];
-            cfor<0, hi>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                load(j, qv[j], qdv[j], qddv[j]);
-            });
-            T cs[hi - lo], sn[hi - lo];
-            V3<T> fn[hi - lo], ff[hi - lo];
-            RneaState<T> st;
-            cfor<0, hi>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                T s_, c_;
-                V3<T> fn_, ff_;
-                if constexpr (j == 0)
-                    rnea_fwd0<T, FAST>(mdl, qv[0], qdv[0], qddv[0], st, s_, c_, fn_, ff_);
-                else
-                    rnea_fwd<T, FAST>(mdl, j, qv[j], qdv[j], qddv[j], st, s_, c_, fn_, ff_);
-                if constexpr (j >= lo) {
-                    sn[j - lo] = s_; cs[j - lo] = c_; fn[j - lo] = fn_; ff[j - lo] = ff_;
-                }
-            });
-            reload_fence();
-            if constexpr (hi < N) rnea_bwd(mdl, hi, ccs, csn, cff, cfn, ff[hi - 1 - lo], fn[hi - 1 - lo]);
-            cfor_rev<hi - lo>([&](auto kc) {
-                constexpr int k = decltype(kc)::value, j = lo + k;
-                out(j, fn[k].z);
-                if constexpr (k > 0) {
-                    rnea_bwd(mdl, j, cs[k], sn[k], ff[k], fn[k], ff[k - 1], fn[k - 1]);
-                } else if constexpr (j > 0) {
-                    ccs = cs[0]; csn = sn[0]; cff = ff[0]; cfn = fn[0];
-                }
-            });
-        }
-    });
-}
-
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-__device__ __forceinline__ void rnea_any(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&qddv)[N],
+RB_HD void rnea_any(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&qddv)[N],
                                          Out &&out) {
     if constexpr (Topo::kSerial)
         rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, static_cast<Out &&>(out));
@@ -188,41 +134,9 @@ __device__ __forceinline__ void rnea_lane(const T *mdl, const T *__restrict__ q,
     rnea_any<T, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
 }
 
-// Segmented lane (model-specialised kernels of long serial chains, tuning rnea_seg): S
-// segments, inputs reloaded per pass (rnea_eval_seg).
-template <typename T, int N, int S, bool FAST>
-__device__ __forceinline__ void rnea_lane_seg(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
-                                              const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b,
-                                              int64_t ld) {
-    const uint32_t off = b * (uint32_t)sizeof(T);
-    rnea_eval_seg<T, N, S, FAST>(
-        mdl,
-        [&](int j, T &x, T &y, T &z) {
-            x = ld_row(q, j * ld, off);
-            y = ld_row(qd, j * ld, off);
-            z = ld_row(qdd, j * ld, off);
-        },
-        [&](int j, T v) { st_row(tau, j * ld, off, v); });
-}
-
-// Paired lane (fp32 model-specialised kernels, spatial.hip.hpp f2): the configurations at
-// lane offset `off` of the batch blocks starting at elements oA and oB, evaluated together.
-template <int N, bool FAST, typename Topo = SerialTopo>
-__device__ __forceinline__ void rnea_lane2(const f2 *mdl, const float *__restrict__ q, const float *__restrict__ qd,
-                                           const float *__restrict__ qdd, float *__restrict__ tau, int64_t oA,
-                                           int64_t oB, uint32_t off, int64_t ld) {
-    f2 qv[N], qdv[N], qddv[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        qv[j] = ld_row2(q, oA, oB, j * ld, off);
-        qdv[j] = ld_row2(qd, oA, oB, j * ld, off);
-        qddv[j] = ld_row2(qdd, oA, oB, j * ld, off);
-    }
-    rnea_any<f2, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, f2 v) { st_row2(tau, oA, oB, j * ld, off, v); });
-}
-
-// Streaming form: walk the batch with `stride`, prefetching the next configuration's
-// joint values into registers before evaluating the current one.
+// Streaming form (precompiled generic kernels, rnea.hip): walk the batch with `stride`,
+// prefetching the next configuration's joint values into registers before evaluating the
+// current one.
 template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void rnea_stream_lane(const T *mdl, const T *__restrict__ q,
                                                  const T *__restrict__ qd, const T *__restrict__ qdd,
@@ -245,83 +159,6 @@ __device__ __forceinline__ void rnea_stream_lane(const T *mdl, const T *__restri
         }
         b = bn;
     }
-}
-
-// ------------------------------------------------------------------ LDS-tiled form
-// A 256-thread block owns configurations [b0, b0+256).  Global traffic moves whole tile
-// rows with 16-byte accesses (one 1 KiB wave-instruction per fp32 row; the probe in
-// probe.hip measures 4-byte lanes at 3.8-3.9 TB/s vs 5.0-5.5 TB/s for 16-byte lanes on
-// this pattern), and the per-lane math keeps one configuration per lane reading its
-// values from LDS (conflict-free: lane t reads word t of a row).
-template <typename T>
-struct Vec16;
-template <>
-struct Vec16<float> {
-    using type = float4;
-};
-template <>
-struct Vec16<double> {
-    using type = double2;
-};
-
-constexpr int kTile = 256;
-
-template <typename T, int ROWS>
-__device__ __forceinline__ void tile_load(const T *__restrict__ a0, const T *__restrict__ a1,
-                                          const T *__restrict__ a2, int rows_per_array, int64_t ld,
-                                          uint32_t b0, T *tile) {
-    using V = typename Vec16<T>::type;
-    constexpr int VPL = 16 / (int)sizeof(T);  // values per 16-byte access
-    constexpr int LPR = kTile / VPL;          // accesses per tile row
-#pragma unroll
-    for (int k0 = 0; k0 < ROWS * LPR; k0 += kTile) {
-        const int k = k0 + (int)threadIdx.x;
-        if (k < ROWS * LPR) {
-            const int r = k / LPR, c = k % LPR;
-            const int arr = r / rows_per_array, j = r % rows_per_array;
-            const T *base = arr == 0 ? a0 : (arr == 1 ? a1 : a2);
-            const V v = *reinterpret_cast<const V *>(base + j * ld + b0 + c * VPL);
-            *reinterpret_cast<V *>(tile + r * kTile + c * VPL) = v;
-        }
-    }
-}
-
-template <typename T, int ROWS>
-__device__ __forceinline__ void tile_store(T *__restrict__ dst, int64_t ld, uint32_t b0, const T *tile) {
-    using V = typename Vec16<T>::type;
-    constexpr int VPL = 16 / (int)sizeof(T);
-    constexpr int LPR = kTile / VPL;
-#pragma unroll
-    for (int k0 = 0; k0 < ROWS * LPR; k0 += kTile) {
-        const int k = k0 + (int)threadIdx.x;
-        if (k < ROWS * LPR) {
-            const int r = k / LPR, c = k % LPR;
-            *reinterpret_cast<V *>(dst + r * ld + b0 + c * VPL) =
-                *reinterpret_cast<const V *>(tile + r * kTile + c * VPL);
-        }
-    }
-}
-
-// Whole-block tile: caller guarantees b0 + 256 <= B and 16-byte alignment of every row
-// start (base pointers and ld * sizeof(T) multiples of 16).  `tile` holds 3N rows.
-template <typename T, int N, bool FAST, typename Topo = SerialTopo>
-__device__ __forceinline__ void rnea_tile(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
-                                          const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b0,
-                                          int64_t ld, T *tile) {
-    const int t = (int)threadIdx.x;
-    tile_load<T, 3 * N>(q, qd, qdd, N, ld, b0, tile);
-    __syncthreads();
-    T qv[N], qdv[N], qddv[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        qv[j] = tile[j * kTile + t];
-        qdv[j] = tile[(N + j) * kTile + t];
-        qddv[j] = tile[(2 * N + j) * kTile + t];
-    }
-    __syncthreads();  // every lane holds its inputs; rows 0..N-1 become the output tile
-    rnea_any<T, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, T v) { tile[j * kTile + t] = v; });
-    __syncthreads();
-    tile_store<T, N>(tau, ld, b0, tile);
 }
 
 }  // namespace dev

@@ -27,11 +27,20 @@ typedef unsigned long long uint64_t;
 
 #include "layout.hpp"
 
+// Per-configuration algebra is host+device: the same lane bodies serve the GPU kernels and
+// the host single-configuration ABI (host_eval.cpp).  Functions that touch device memory
+// spaces or GPU-only builtins (row access, LDS staging, hardware reciprocal) stay __device__.
+#if defined(__HIPCC_RTC__)
+#define RB_HD __device__ __forceinline__
+#else
+#define RB_HD __host__ __device__ __forceinline__
+#endif
+
 namespace rbamd {
 namespace dev {
 
-__device__ __forceinline__ float fmadd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ double fmadd(double a, double b, double c) { return __builtin_fma(a, b, c); }
+RB_HD float fmadd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+RB_HD double fmadd(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 // Paired fp32 lanes (model-specialised fp32 kernels, tuning `pack`): a lane evaluates two
 // configurations at once as a 2-wide vector, so every FMA/MUL/ADD of the recursion becomes
@@ -41,7 +50,7 @@ __device__ __forceinline__ double fmadd(double a, double b, double c) { return _
 // §4), not for the memory-bound RNEA.  Only sin/cos and 1/x stay per element; both halves run
 // identical instruction sequences.
 typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 fmadd(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+RB_HD f2 fmadd(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 template <typename T>
 struct V3 {
@@ -49,24 +58,24 @@ struct V3 {
 };
 
 template <typename T>
-__device__ __forceinline__ V3<T> v3(T x, T y, T z) { return V3<T>{x, y, z}; }
+RB_HD V3<T> v3(T x, T y, T z) { return V3<T>{x, y, z}; }
 
 // a x b
 template <typename T>
-__device__ __forceinline__ V3<T> cross(const V3<T> &a, const V3<T> &b) {
+RB_HD V3<T> cross(const V3<T> &a, const V3<T> &b) {
     return v3(fmadd(a.y, b.z, -a.z * b.y), fmadd(a.z, b.x, -a.x * b.z), fmadd(a.x, b.y, -a.y * b.x));
 }
 
 // acc + a x b
 template <typename T>
-__device__ __forceinline__ V3<T> cross_add(const V3<T> &acc, const V3<T> &a, const V3<T> &b) {
+RB_HD V3<T> cross_add(const V3<T> &acc, const V3<T> &a, const V3<T> &b) {
     return v3(fmadd(a.y, b.z, fmadd(-a.z, b.y, acc.x)), fmadd(a.z, b.x, fmadd(-a.x, b.z, acc.y)),
               fmadd(a.x, b.y, fmadd(-a.y, b.x, acc.z)));
 }
 
 // acc - a x b
 template <typename T>
-__device__ __forceinline__ V3<T> cross_sub(const V3<T> &acc, const V3<T> &a, const V3<T> &b) {
+RB_HD V3<T> cross_sub(const V3<T> &acc, const V3<T> &a, const V3<T> &b) {
     return v3(fmadd(-a.y, b.z, fmadd(a.z, b.y, acc.x)), fmadd(-a.z, b.x, fmadd(a.x, b.z, acc.y)),
               fmadd(-a.x, b.y, fmadd(a.y, b.x, acc.z)));
 }
@@ -79,7 +88,7 @@ struct M3 {
 
 // M x
 template <typename T>
-__device__ __forceinline__ V3<T> mul(const M3<T> &M, const V3<T> &x) {
+RB_HD V3<T> mul(const M3<T> &M, const V3<T> &x) {
     return v3(fmadd(M.m[0], x.x, fmadd(M.m[1], x.y, M.m[2] * x.z)),
               fmadd(M.m[3], x.x, fmadd(M.m[4], x.y, M.m[5] * x.z)),
               fmadd(M.m[6], x.x, fmadd(M.m[7], x.y, M.m[8] * x.z)));
@@ -87,7 +96,7 @@ __device__ __forceinline__ V3<T> mul(const M3<T> &M, const V3<T> &x) {
 
 // acc + M x
 template <typename T>
-__device__ __forceinline__ V3<T> mul_add(const V3<T> &acc, const M3<T> &M, const V3<T> &x) {
+RB_HD V3<T> mul_add(const V3<T> &acc, const M3<T> &M, const V3<T> &x) {
     return v3(fmadd(M.m[0], x.x, fmadd(M.m[1], x.y, fmadd(M.m[2], x.z, acc.x))),
               fmadd(M.m[3], x.x, fmadd(M.m[4], x.y, fmadd(M.m[5], x.z, acc.y))),
               fmadd(M.m[6], x.x, fmadd(M.m[7], x.y, fmadd(M.m[8], x.z, acc.z))));
@@ -95,7 +104,7 @@ __device__ __forceinline__ V3<T> mul_add(const V3<T> &acc, const M3<T> &M, const
 
 // M^T x
 template <typename T>
-__device__ __forceinline__ V3<T> mul_t(const M3<T> &M, const V3<T> &x) {
+RB_HD V3<T> mul_t(const M3<T> &M, const V3<T> &x) {
     return v3(fmadd(M.m[0], x.x, fmadd(M.m[3], x.y, M.m[6] * x.z)),
               fmadd(M.m[1], x.x, fmadd(M.m[4], x.y, M.m[7] * x.z)),
               fmadd(M.m[2], x.x, fmadd(M.m[5], x.y, M.m[8] * x.z)));
@@ -108,14 +117,14 @@ struct S3 {
 };
 
 template <typename T>
-__device__ __forceinline__ V3<T> mul(const S3<T> &S, const V3<T> &x) {
+RB_HD V3<T> mul(const S3<T> &S, const V3<T> &x) {
     return v3(fmadd(S.xx, x.x, fmadd(S.xy, x.y, S.xz * x.z)),
               fmadd(S.xy, x.x, fmadd(S.yy, x.y, S.yz * x.z)),
               fmadd(S.xz, x.x, fmadd(S.yz, x.y, S.zz * x.z)));
 }
 
 template <typename T>
-__device__ __forceinline__ V3<T> mul_add(const V3<T> &acc, const S3<T> &S, const V3<T> &x) {
+RB_HD V3<T> mul_add(const V3<T> &acc, const S3<T> &S, const V3<T> &x) {
     return v3(fmadd(S.xx, x.x, fmadd(S.xy, x.y, fmadd(S.xz, x.z, acc.x))),
               fmadd(S.xy, x.x, fmadd(S.yy, x.y, fmadd(S.yz, x.z, acc.y))),
               fmadd(S.xz, x.x, fmadd(S.yz, x.y, fmadd(S.zz, x.z, acc.z))));
@@ -187,16 +196,16 @@ __device__ __forceinline__ void stage_model(const T *__restrict__ mdl, T *smem) 
 #define RB_OPAQUE_CONSTS 0
 #endif
 template <typename T>
-__device__ __forceinline__ T mconst(T v) {
+RB_HD T mconst(T v) {
     if constexpr (RB_OPAQUE_CONSTS != 0) {
         if (__builtin_constant_p(v) && v != T(0) && v != T(1) && v != T(-1)) asm volatile("" : "+s"(v));
     }
     return v;
 }
-__device__ __forceinline__ f2 mconst(f2 v) { return v; }  // paired kernels do not pin constants
+RB_HD f2 mconst(f2 v) { return v; }  // paired kernels do not pin constants
 
 template <typename T>
-__device__ __forceinline__ Link<T> load_link(const T *__restrict__ mdl, int i) {
+RB_HD Link<T> load_link(const T *__restrict__ mdl, int i) {
     const T *c = mdl + i * kLinkStride;
     Link<T> L;
 #pragma unroll
@@ -211,7 +220,7 @@ __device__ __forceinline__ Link<T> load_link(const T *__restrict__ mdl, int i) {
 
 // E = R_p * Rz(q): columns 0/1 mix with (cos, sin), column 2 is R_p's.
 template <typename T>
-__device__ __forceinline__ M3<T> joint_rotation(const M3<T> &Rp, T c, T s) {
+RB_HD M3<T> joint_rotation(const M3<T> &Rp, T c, T s) {
     M3<T> E;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -225,7 +234,7 @@ __device__ __forceinline__ M3<T> joint_rotation(const M3<T> &Rp, T c, T s) {
 
 // Rigid-body inertia times a motion vector (inertia.rs:107-117); returns (rot, lin).
 template <typename T>
-__device__ __forceinline__ void inertia_mul(const Link<T> &L, const V3<T> &w, const V3<T> &v,
+RB_HD void inertia_mul(const Link<T> &L, const V3<T> &w, const V3<T> &v,
                                             V3<T> &n, V3<T> &f) {
     n = cross_add(mul(L.Io, w), L.h, v);                     // I_o w + h x v
     f = cross_sub(v3(L.m * v.x, L.m * v.y, L.m * v.z), L.h, w);  // m v - h x w
@@ -285,7 +294,7 @@ __device__ __forceinline__ void st_row(T *__restrict__ base, int64_t row, uint32
 
 // Compiler-only fence: forces per-link constants to be re-read from LDS in a later
 // sweep instead of being kept live in VGPRs across the whole chain.
-__device__ __forceinline__ void reload_fence() { asm volatile("" ::: "memory"); }
+RB_HD void reload_fence() { asm volatile("" ::: "memory"); }
 
 // ---------------------------------------------------------------------------- sincos
 // Joint angles need sin/cos once per link.  The ROCm device-library sincos carries a
@@ -295,7 +304,7 @@ __device__ __forceinline__ void reload_fence() { asm volatile("" ::: "memory"); 
 // __kernel_sin/__kernel_cos minimax polynomials on |r| <= pi/4 (<= 1 ulp for
 // |x| < 2^20 rad -- far beyond any joint angle).  FAST=true (fp32 only) uses the
 // hardware v_sin_f32/v_cos_f32.
-__device__ __forceinline__ void sincos_cw(double x, double &s, double &c) {
+RB_HD void sincos_cw(double x, double &s, double &c) {
     const double k = __builtin_rint(x * 6.36619772367581382433e-01);  // 2/pi
     double r = __builtin_fma(-k, 1.57079632679489655800e+00, x);      // pi/2 hi
     r = __builtin_fma(-k, 6.12323399573676603587e-17, r);              // pi/2 mid
@@ -321,7 +330,7 @@ __device__ __forceinline__ void sincos_cw(double x, double &s, double &c) {
     c = ((q + 1) & 2) ? -cc : cc;
 }
 
-__device__ __forceinline__ void sincos_cw(float x, float &s, float &c) {
+RB_HD void sincos_cw(float x, float &s, float &c) {
     const float k = __builtin_rintf(x * 6.3661977236e-01f);
     float r = __builtin_fmaf(-k, 1.57079637e+00f, x);
     r = __builtin_fmaf(-k, -4.37113883e-08f, r);
@@ -339,7 +348,7 @@ __device__ __forceinline__ void sincos_cw(float x, float &s, float &c) {
 }
 
 template <bool FAST>
-__device__ __forceinline__ void sin_cos(float x, float &s, float &c) {
+RB_HD void sin_cos(float x, float &s, float &c) {
     if constexpr (FAST) {
         __sincosf(x, &s, &c);
     } else {
@@ -393,7 +402,7 @@ __device__ __forceinline__ void sincos_tab(double x, double &s, double &c) {
 #endif
 
 template <bool FAST>
-__device__ __forceinline__ void sin_cos(double x, double &s, double &c) {
+RB_HD void sin_cos(double x, double &s, double &c) {
 #if RB_SINCOS_TAB
     sincos_tab(x, s, c);
 #else
@@ -401,7 +410,7 @@ __device__ __forceinline__ void sin_cos(double x, double &s, double &c) {
 #endif
 }
 template <bool FAST>
-__device__ __forceinline__ void sin_cos(f2 x, f2 &s, f2 &c) {
+RB_HD void sin_cos(f2 x, f2 &s, f2 &c) {
     float s0, c0, s1, c1;
     sin_cos<FAST>(x.x, s0, c0);
     sin_cos<FAST>(x.y, s1, c1);

@@ -32,7 +32,7 @@ struct IC {
 };
 
 template <int I, int N, typename F>
-__device__ __forceinline__ void cfor(F &&f) {
+RB_HD void cfor(F &&f) {
     if constexpr (I < N) {
         f(IC<I>{});
         cfor<I + 1, N>(f);
@@ -41,7 +41,7 @@ __device__ __forceinline__ void cfor(F &&f) {
 
 // f(I-1), f(I-2), ..., f(0)
 template <int I, typename F>
-__device__ __forceinline__ void cfor_rev(F &&f) {
+RB_HD void cfor_rev(F &&f) {
     if constexpr (I > 0) {
         f(IC<I - 1>{});
         cfor_rev<I - 1>(f);
@@ -52,7 +52,7 @@ __device__ __forceinline__ void cfor_rev(F &&f) {
 // r = p + R_p e_z q for a prismatic one (the model packer has already turned every joint
 // axis into local z, model.cpp pack).
 template <typename T, bool PRISMATIC>
-__device__ __forceinline__ void link_frame(const Link<T> &L, T q, T c, T s, M3<T> &E, V3<T> &r) {
+RB_HD void link_frame(const Link<T> &L, T q, T c, T s, M3<T> &E, V3<T> &r) {
     if constexpr (PRISMATIC) {
         E = L.Rp;
         r = v3(fmadd(L.Rp.m[2], q, L.p.x), fmadd(L.Rp.m[5], q, L.p.y), fmadd(L.Rp.m[8], q, L.p.z));
@@ -63,12 +63,12 @@ __device__ __forceinline__ void link_frame(const Link<T> &L, T q, T c, T s, M3<T
 }
 
 template <typename T>
-__device__ __forceinline__ V3<T> add3(const V3<T> &a, const V3<T> &b) {
+RB_HD V3<T> add3(const V3<T> &a, const V3<T> &b) {
     return v3(a.x + b.x, a.y + b.y, a.z + b.z);
 }
 
 template <typename T>
-__device__ __forceinline__ void add_art(ArtI<T> &I, const ArtI<T> &J) {
+RB_HD void add_art(ArtI<T> &I, const ArtI<T> &J) {
     I.A = S3<T>{I.A.xx + J.A.xx, I.A.xy + J.A.xy, I.A.xz + J.A.xz, I.A.yy + J.A.yy, I.A.yz + J.A.yz, I.A.zz + J.A.zz};
 #pragma unroll
     for (int k = 0; k < 9; ++k) I.B.m[k] += J.B.m[k];
@@ -78,7 +78,7 @@ __device__ __forceinline__ void add_art(ArtI<T> &I, const ArtI<T> &J) {
 // Child -> parent force transform (spatial.rs:242-248 with the isometry inverse):
 // f' = E f,  n' = E n + r x f'
 template <typename T>
-__device__ __forceinline__ void force_to_parent(const M3<T> &E, const V3<T> &r, V3<T> &n, V3<T> &f) {
+RB_HD void force_to_parent(const M3<T> &E, const V3<T> &r, V3<T> &n, V3<T> &f) {
     const V3<T> fl = mul(E, f);
     n = cross_add(mul(E, n), r, fl);
     f = fl;
@@ -86,7 +86,7 @@ __device__ __forceinline__ void force_to_parent(const M3<T> &E, const V3<T> &r, 
 
 // ----------------------------------------------------------------------------- RNEA
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-__device__ __forceinline__ void rnea_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
+RB_HD void rnea_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
                                                const T (&qddv)[N], Out &&out) {
     T cs[N], sn[N];
     V3<T> W[N], V[N], AW[N], AV[N];  // link velocity / acceleration (rot, lin), link coordinates
@@ -163,7 +163,7 @@ __device__ __forceinline__ void rnea_eval_tree(const T *mdl, const T (&qv)[N], c
 // projected inertia I^a = I^A - U U^T / D annihilates S, so the corresponding row/column
 // is written as exact zeros (as the serial kernel does).
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-__device__ __forceinline__ void aba_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
+RB_HD void aba_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
                                               Out &&out) {
     T cs[N], sn[N];
     V3<T> W[N], V[N];                  // pass-1 velocities (read by children)
@@ -324,7 +324,7 @@ __device__ __forceinline__ void aba_eval_tree(const T *mdl, const T (&qv)[N], co
 // Output as crba_body.hip.hpp: element row + N*col of the column-major matrix, upper
 // triangle; strictly-lower entries and non-ancestor pairs exact zeros.
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-__device__ __forceinline__ void crba_eval_tree(const T *mdl, const T (&qv)[N], Out &&out) {
+RB_HD void crba_eval_tree(const T *mdl, const T (&qv)[N], Out &&out) {
     T cs[N], sn[N];
     cfor<0, N>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
@@ -384,7 +384,7 @@ __device__ __forceinline__ void crba_eval_tree(const T *mdl, const T (&qv)[N], O
 // (multibody.rs:95-108, body Jacobian of the last link, rows [lin; rot], 6 x N column-major)
 // along the last link's ancestor path.
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-__device__ __forceinline__ void fwd_kin_tree(const T *mdl, const T (&qv)[N], Out &&out) {
+RB_HD void fwd_kin_tree(const T *mdl, const T (&qv)[N], Out &&out) {
     M3<T> R{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
     V3<T> p = v3(T(0), T(0), T(0));
     cfor<0, N>([&](auto jc) {
@@ -412,7 +412,7 @@ __device__ __forceinline__ void fwd_kin_tree(const T *mdl, const T (&qv)[N], Out
 }
 
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-__device__ __forceinline__ void jac_tree(const T *mdl, const T (&qv)[N], Out &&out) {
+RB_HD void jac_tree(const T *mdl, const T (&qv)[N], Out &&out) {
     // acc = pose of the last frame in frame i, leaf -> root, starting from the model tail
     // (the last link's axis-frame change, layout.hpp kTailOut)
     M3<T> R;

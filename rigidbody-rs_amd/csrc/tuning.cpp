@@ -4,8 +4,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
+#include <string>
 #include <utility>
 
 namespace rbamd {
@@ -17,27 +19,60 @@ int env_int(const char *name, int dflt) {
 }
 }  // namespace
 
+bool tuning_experimental() {
+    static const bool on = env_int("RB_EXPERIMENTAL", 0) != 0;
+    return on;
+}
+
+namespace {
+struct Key {
+    const char *name;
+    int Tuning::*field;
+    bool experimental;
+};
+const Key kKeys[] = {
+    {"jit", &Tuning::jit, false},
+    {"pack", &Tuning::pack, false},
+    {"rnea_stream", &Tuning::rnea_stream, false},
+    {"single_gpu", &Tuning::single_gpu, false},
+    {"grid_factor", &Tuning::grid_factor, true},
+    {"rnea_nt", &Tuning::rnea_nt, true},
+    {"fd_nt", &Tuning::fd_nt, true},
+    {"jit_waves", &Tuning::jit_waves, true},
+    {"opaque_consts", &Tuning::opaque_consts, true},
+    {"f64_tab", &Tuning::f64_tab, true},
+    {"split_rot", &Tuning::split_rot, true},
+    {"jit_variant", &Tuning::jit_variant, true},
+};
+
+// RB_<KEY> environment overrides (upper-cased key), experimental ones only with RB_EXPERIMENTAL=1.
+void from_env(Tuning &t) {
+    for (const Key &k : kKeys) {
+        if (k.experimental && !tuning_experimental()) continue;
+        std::string var = "RB_";
+        for (const char *c = k.name; *c; ++c) var += (char)(*c >= 'a' && *c <= 'z' ? *c - 32 : *c);
+        t.*(k.field) = env_int(var.c_str(), t.*(k.field));
+    }
+}
+}  // namespace
+
 Tuning &tuning() {
     static Tuning t = [] {
         Tuning x;
-        x.rnea_stream = env_int("RB_RNEA_STREAM", x.rnea_stream);
-        x.grid_factor = env_int("RB_GRID_FACTOR", x.grid_factor);
-        x.jit = env_int("RB_JIT", x.jit);
-        x.rnea_tile = env_int("RB_RNEA_TILE", x.rnea_tile);
-        x.rnea_nt = env_int("RB_RNEA_NT", x.rnea_nt);
-        x.fd_nt = env_int("RB_FD_NT", x.fd_nt);
-        x.opaque_consts = env_int("RB_OPAQUE_CONSTS", x.opaque_consts);
-        x.fd_stream = env_int("RB_FD_STREAM", x.fd_stream);
-        x.jit_waves = env_int("RB_JIT_WAVES", x.jit_waves);
-        x.jit_variant = env_int("RB_JIT_VARIANT", x.jit_variant);
-        x.pack = env_int("RB_PACK", x.pack);
-        x.f64_tab = env_int("RB_F64_TAB", x.f64_tab);
-        x.rnea_seg = env_int("RB_RNEA_SEG", x.rnea_seg);
-        x.rnea_tiles = env_int("RB_RNEA_TILES", x.rnea_tiles);
-        x.split_rot = env_int("RB_SPLIT_ROT", x.split_rot);
+        from_env(x);
         return x;
     }();
     return t;
+}
+
+int tuning_set(const char *key, int value) {
+    for (const Key &k : kKeys) {
+        if (std::strcmp(k.name, key) != 0) continue;
+        if (k.experimental && !tuning_experimental()) return 2;
+        tuning().*(k.field) = value;
+        return 0;
+    }
+    return 1;
 }
 
 unsigned stream_grid(const void *kfn, int block, unsigned full, int factor) {

@@ -1,19 +1,33 @@
 // tuning.hpp -- launch-shape knobs (host side) and resident-grid sizing.
+//
+// Production knobs (rb_set_tuning accepts these always): `jit`, `pack`, `rnea_stream`,
+// `single_gpu`.
+// Everything else is an A/B experiment selector: rb_set_tuning accepts it only when the
+// process runs with RB_EXPERIMENTAL=1 (tools/ab_bench.py, tools/small_batch.py), so a normal
+// caller cannot multiply the hipRTC kernel variants (jit.cpp cache key) or the test matrix.
 #pragma once
 
 namespace rbamd {
 
 struct Tuning {
-    // RNEA launch form: 1 grid-stride + register prefetch, 0 one configuration per lane,
-    // -1 auto (measured on MI355X: one-per-lane for fp32 up to 8 DOF, streaming for fp64
-    // and longer chains -- tools/ab_bench.py).
+    // ---- production
+    int jit = 1;  // 1: model-specialised hipRTC kernels where available (jit.hpp)
+    // JIT fp32 forward dynamics: 2 = two configurations per lane on packed fp32
+    // (spatial.hip.hpp f2; 512 configurations per 256-lane block), 1 = one per lane,
+    // -1 auto (jit_pack in jit.cpp: chains up to 8 links, batches >= 2^18).
+    int pack = -1;
+    // Precompiled (generic) RNEA launch form: 1 grid-stride + register prefetch, 0 one
+    // configuration per lane, -1 auto (streaming for fp64 and chains longer than 8 links,
+    // where it measured 7-9% faster -- DESIGN.md §4).  The model-specialised kernels are
+    // always one configuration per lane.
     int rnea_stream = -1;
+    // Single-configuration ABI (multibody_rnea / _crba / _fwd_kin / _jac): 0 = on the calling
+    // host thread with the lane bodies compiled for the host (host_eval.cpp) where the model
+    // allows it, 1 = always a GPU launch (H2D, kernel, D2H, sync).
+    int single_gpu = 0;
+
+    // ---- experimental (RB_EXPERIMENTAL=1)
     int grid_factor = 1;  // streaming grid = grid_factor x resident blocks (capped by the batch)
-    int jit = 1;          // 1: model-specialised hipRTC kernels where available (jit.hpp)
-    // 1: LDS-tiled 16-byte-access form of the JIT RNEA kernel when aligned.  Off: it is
-    // 30% slower than the per-lane form on MI355X (block barriers serialise load/compute/
-    // store; the per-lane form already runs at the pattern's copy ceiling).
-    int rnea_tile = 0;
     // JIT RNEA: bit 0 non-temporal loads, bit 1 non-temporal stores (every element is
     // touched once; measured -5% fp32 / -8% fp64 kernel time).
     int rnea_nt = 3;
@@ -25,25 +39,12 @@ struct Tuning {
     int jit_waves = -1;
     // Model constants pinned per use (spatial.hip.hpp mconst): 1 on, 0 off, -1 auto = the
     // rollout of chains up to 16 links (fp32 337 vs 1736 us; fp64 810 vs 995 us); off for
-    // forward dynamics (fp32 29.6 vs 31.9 us once the 1/D reciprocal freed 12 VGPRs -- it
-    // was 33.8 vs 35.7 the other way before; fp64 71 vs 90 us; 30-link fp32 333 vs 1331 us)
+    // forward dynamics (fp32 29.6 vs 31.9 us; fp64 71 vs 90 us; 30-link fp32 333 vs 1331 us)
     // and for the other kinds.
     int opaque_consts = -1;
-    // JIT forward dynamics: 1 = resident grid-stride form with register prefetch (aba_stream).
-    int fd_stream = 0;
-    // JIT fp32 RNEA / forward dynamics: 1 = two configurations per lane on packed fp32
-    // (spatial.hip.hpp f2; 512 configurations per 256-lane block), 0 = one per lane,
-    // -1 auto (jit_pack in jit.cpp).
-    int pack = -1;
     // JIT fp64 kernels: 1 = table-assisted sincos (spatial.hip.hpp sincos_tab), 0 = the
     // pi/2-reduction minimax sincos_cw, -1 auto (on).
     int f64_tab = -1;
-    // JIT RNEA of serial chains: segments of the segmented form (rnea_eval_seg); 0/1 = the
-    // one-pass form, -1 auto (jit_rnea_seg in jit.cpp).
-    int rnea_seg = -1;
-    // JIT RNEA lane kernel (one configuration per lane): 256-configuration tiles per
-    // workgroup (1, 2 or 4 -> 256 / 512 / 1024 threads).
-    int rnea_tiles = 1;
     // JIT ABA / CRBA: rotate symmetric inertia blocks as R_p (Rz S Rz^T) R_p^T with the double
     // angle (artinertia.hip.hpp to_parent_split); 0 = the folded E S E^T; -1 auto = on when
     // every joint frame R_p is a signed permutation.
@@ -52,22 +53,26 @@ struct Tuning {
     int jit_variant = 0;
 };
 
-// Process-wide knobs, initialised from RB_RNEA_STREAM / RB_GRID_FACTOR / RB_JIT, adjustable through
-// rb_set_tuning() (used by the A/B benchmarks; not needed for normal use).
+// Process-wide knobs, initialised from RB_JIT / RB_PACK / RB_RNEA_STREAM (and, with
+// RB_EXPERIMENTAL=1, the experimental RB_* variables), adjustable through rb_set_tuning().
 Tuning &tuning();
+
+// Whether RB_EXPERIMENTAL=1 is set (experimental knobs writable).
+bool tuning_experimental();
+
+// Sets `key`; returns 0, 1 (unknown key) or 2 (experimental key without RB_EXPERIMENTAL=1).
+int tuning_set(const char *key, int value);
 
 // Blocks for a streaming launch of `kfn`: factor x (resident blocks per CU x CUs) on the
 // current device, never more than `full` (one block per 256 configurations).  Cached per
 // (device, kernel).
 unsigned stream_grid(const void *kfn, int block, unsigned full, int factor);
 
-// RNEA launch form.  Measured (tools/ab_bench.py): for the precompiled
-// generic kernels the streaming form wins for fp64 and chains longer than 8 links; the
-// model-specialised (JIT) kernels are lighter and the one-per-lane form wins everywhere.
-inline bool rnea_use_stream(bool f64, int n, bool jit) {
+// RNEA launch form of the precompiled kernels (the JIT kernels are one per lane).
+inline bool rnea_use_stream(bool f64, int n) {
     const int v = tuning().rnea_stream;
     if (v >= 0) return v != 0;
-    return jit ? false : (f64 || n > 8);
+    return f64 || n > 8;
 }
 
 }  // namespace rbamd

@@ -5,7 +5,8 @@ Host-side mirror of the reference's interface for the hot path:
 * `Multibody.new()` / `.from_urdf(path)` / `.from_urdf_string(xml)` <- `multibody_new`,
   `Multibody::from_urdf` (rigidbody_bindings/src/lib.rs:8-12, multibody.rs:65-77)
 * `.rnea(q, dq, ddq)`, `.crba(q)`, `.fwd_kin(q)`, `.jac(q)` <- the single-config C ABI
-  (lib.rs:15-70), same argument meaning and result layout; computed on the GPU
+  (lib.rs:15-70), same argument meaning and result layout; computed on the calling thread
+  with the GPU lane bodies compiled for the host (`.single_config_path()`), or on the GPU
 * `.rnea_batch`, `.fd_batch`, `.crba_batch`, `.fwd_kin_batch`, `.jac_batch` <- batched
   device-pointer entry points on torch CUDA tensors laid out [n, B] (SoA)
 
@@ -81,6 +82,7 @@ _sig("multibody_fwd_kin_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _v
 _sig("multibody_jac_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_rnea_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
 _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
+_sig("multibody_single_config_path", ctypes.c_int, [_vp])
 _sig("multibody_kernel_path", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int])
 _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
@@ -125,7 +127,8 @@ def supported_dofs():
 
 
 def set_tuning(key: str, value: int):
-    """rb_set_tuning: process-wide launch knobs ("rnea_stream", "grid_factor", "jit")."""
+    """rb_set_tuning: process-wide knobs -- production "jit", "pack", "rnea_stream",
+    "single_gpu"; the A/B selectors only with RB_EXPERIMENTAL=1 (csrc/tuning.hpp)."""
     _check(_lib.rb_set_tuning(key.encode(), int(value)), f"set_tuning({key})")
 
 
@@ -152,10 +155,32 @@ def _take(ptr, count):
 _TORCH_SUFFIX = {torch.float32: "f32", torch.float64: "f64"}
 
 
-def _stream_ptr(stream):
+def _stream_ptr(stream, device=None):
+    """The HIP stream a call is enqueued on: `stream`, else the current stream of `device`."""
     if stream is None:
-        stream = torch.cuda.current_stream()
+        stream = torch.cuda.current_stream(device)
+    elif device is not None and stream.device != device:
+        raise ValueError(f"stream is on {stream.device}, the arrays on {device}")
     return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _one_device(ts):
+    """All arrays of one call must live on one device: the library uploads the model and
+    launches on the CURRENT device (hipGetDevice), so the caller makes it theirs
+    (`with torch.cuda.device(dev)` around the call)."""
+    devs = {t.device for t in ts}
+    if len(devs) != 1:
+        raise ValueError(f"all arrays of one call must be on one device, got {sorted(map(str, devs))}")
+    return devs.pop()
+
+
+def _host_soa(arrs, n):
+    """[n, B] float64 host arrays of one batched host call: same shape, n rows."""
+    out = [np.ascontiguousarray(x, dtype=np.float64) for x in arrs]
+    for a in out:
+        if a.ndim != 2 or a.shape[0] != n or a.shape != out[0].shape:
+            raise ValueError(f"host batch arrays must all be [{n}, B], got {[x.shape for x in out]}")
+    return out
 
 
 def _soa(t, n, name, dtype=None, B=None):
@@ -187,6 +212,14 @@ def _same_ld(ts):
     if len(lds) != 1:
         raise ValueError("all [n, B] arrays of one call must share the leading dimension")
     return lds.pop()
+
+
+def _kin_out(out, rows, q):
+    """Output of fwd_kin / jac batches: [rows, B] float64 with the input's leading dimension."""
+    B = q.shape[1]
+    if not isinstance(out, torch.Tensor) or out.dtype != torch.float64 or tuple(out.shape) != (rows, B) or \
+            (B > 1 and (out.stride(1) != 1 or out.stride(0) != _ld(q))):
+        raise ValueError(f"out must be a float64 [{rows}, {B}] tensor with the input's leading dimension")
 
 
 class Multibody:
@@ -274,6 +307,14 @@ class Multibody:
             raise RigidBodyError(last_error())
         return "jit" if r == 1 else "generic"
 
+    def single_config_path(self) -> str:
+        """'host' when the single-configuration queries (rnea, crba, fwd_kin, jac) run on the
+        calling thread (host_eval.cpp), 'gpu' when each is a GPU launch."""
+        r = _lib.multibody_single_config_path(self._h)
+        if r < 0:
+            raise RigidBodyError(last_error())
+        return "host" if r == 0 else "gpu"
+
     def rnea_kernel_path(self, f64=False) -> str:
         return self.kernel_path("rnea", f64)
 
@@ -324,9 +365,11 @@ class Multibody:
             out = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
         _soa(out, self.n, "tau", q.dtype, B)
         ld = _same_ld((q, qd, qdd, out))
+        dev = _one_device((q, qd, qdd, out))
         fn = getattr(_lib, f"multibody_rnea_batch_{_TORCH_SUFFIX[q.dtype]}")
-        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), qdd.data_ptr(), out.data_ptr(), B, ld,
-                  _stream_ptr(stream)), "rnea_batch")
+        with torch.cuda.device(dev):
+            _check(fn(self._h, q.data_ptr(), qd.data_ptr(), qdd.data_ptr(), out.data_ptr(), B, ld,
+                      _stream_ptr(stream, dev)), "rnea_batch")
         return out
 
     def fd_batch(self, q, qd, tau, out=None, stream=None):
@@ -338,9 +381,11 @@ class Multibody:
             out = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device)
         _soa(out, self.n, "qdd", q.dtype, B)
         ld = _same_ld((q, qd, tau, out))
+        dev = _one_device((q, qd, tau, out))
         fn = getattr(_lib, f"multibody_fd_batch_{_TORCH_SUFFIX[q.dtype]}")
-        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), out.data_ptr(), B, ld,
-                  _stream_ptr(stream)), "fd_batch")
+        with torch.cuda.device(dev):
+            _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), out.data_ptr(), B, ld,
+                      _stream_ptr(stream, dev)), "fd_batch")
         return out
 
     # ---- tiled layout [ceil(B/256), n, 256] (rigidbody_batch.h) ----------------------
@@ -358,9 +403,11 @@ class Multibody:
         a = self._tiled(a, "arg0", B)
         b, c = self._tiled(b, "arg1", B, a.dtype), self._tiled(c, "arg2", B, a.dtype)
         out = torch.empty_like(a) if out is None else self._tiled(out, "out", B, a.dtype)
+        dev = _one_device((a, b, c, out))
         fn = getattr(_lib, f"multibody_{kind}_batch_tiled_{_TORCH_SUFFIX[a.dtype]}")
-        _check(fn(self._h, a.data_ptr(), b.data_ptr(), c.data_ptr(), out.data_ptr(), B, _stream_ptr(stream)),
-               f"{kind}_batch_tiled")
+        with torch.cuda.device(dev):
+            _check(fn(self._h, a.data_ptr(), b.data_ptr(), c.data_ptr(), out.data_ptr(), B,
+                      _stream_ptr(stream, dev)), f"{kind}_batch_tiled")
         return out
 
     def rnea_batch_tiled(self, q, qd, qdd, B, out=None, stream=None):
@@ -386,9 +433,12 @@ class Multibody:
             raise ValueError("rollout needs contiguous [n, B] state (ld == B), like tau_seq")
         K = tau_seq.shape[0]
         tr = torch.empty_like(tau_seq) if traj else None
+        dev = _one_device((q, qd, tau_seq))
         fn = getattr(_lib, f"multibody_rollout_batch_{_TORCH_SUFFIX[q.dtype]}")
-        _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau_seq.data_ptr(), float(dt), int(K),
-                  tr.data_ptr() if tr is not None else None, B, max(ld, B, 1), _stream_ptr(stream)), "rollout_batch")
+        with torch.cuda.device(dev):
+            _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau_seq.data_ptr(), float(dt), int(K),
+                      tr.data_ptr() if tr is not None else None, B, max(ld, B, 1), _stream_ptr(stream, dev)),
+                   "rollout_batch")
         return tr
 
     def crba_batch(self, q, out=None, stream=None):
@@ -399,7 +449,9 @@ class Multibody:
         fn = getattr(_lib, f"multibody_crba_batch_{_TORCH_SUFFIX[q.dtype]}")
         if out.shape != (self.n * self.n, B) or (B > 1 and out.stride(0) != _ld(q)):
             raise ValueError("out must be [n*n, B] with the inputs' leading dimension")
-        _check(fn(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q), _stream_ptr(stream)), "crba_batch")
+        dev = _one_device((q, out))
+        with torch.cuda.device(dev):
+            _check(fn(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q), _stream_ptr(stream, dev)), "crba_batch")
         return out
 
     def fwd_kin_batch(self, q, out=None, stream=None):
@@ -407,8 +459,11 @@ class Multibody:
         B = q.shape[1]
         if out is None:
             out = torch.empty((3, _ld(q)), dtype=q.dtype, device=q.device)[:, :B]
-        _check(_lib.multibody_fwd_kin_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q),
-                                                _stream_ptr(stream)), "fwd_kin_batch")
+        _kin_out(out, 3, q)
+        dev = _one_device((q, out))
+        with torch.cuda.device(dev):
+            _check(_lib.multibody_fwd_kin_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q),
+                                                    _stream_ptr(stream, dev)), "fwd_kin_batch")
         return out
 
     def jac_batch(self, q, out=None, stream=None):
@@ -416,13 +471,16 @@ class Multibody:
         B = q.shape[1]
         if out is None:
             out = torch.empty((6 * self.n, _ld(q)), dtype=q.dtype, device=q.device)[:, :B]
-        _check(_lib.multibody_jac_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q),
-                                            _stream_ptr(stream)), "jac_batch")
+        _kin_out(out, 6 * self.n, q)
+        dev = _one_device((q, out))
+        with torch.cuda.device(dev):
+            _check(_lib.multibody_jac_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q),
+                                                _stream_ptr(stream, dev)), "jac_batch")
         return out
 
     # -------------------------------------------------------- batched, host [n, B]
     def rnea_batch_host(self, q, qd, qdd):
-        arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (q, qd, qdd)]
+        arrs = _host_soa((q, qd, qdd), self.n)
         B = arrs[0].shape[1]
         out = np.empty_like(arrs[0])
         _check(_lib.multibody_rnea_batch_host_f64(self._h, *[a.ctypes.data_as(_dp) for a in arrs],
@@ -430,7 +488,7 @@ class Multibody:
         return out
 
     def fd_batch_host(self, q, qd, tau):
-        arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (q, qd, tau)]
+        arrs = _host_soa((q, qd, tau), self.n)
         B = arrs[0].shape[1]
         out = np.empty_like(arrs[0])
         _check(_lib.multibody_fd_batch_host_f64(self._h, *[a.ctypes.data_as(_dp) for a in arrs],
@@ -445,7 +503,8 @@ def to_tiled(x, stream=None):
     rows, B = x.shape
     out = torch.empty(((B + TILE - 1) // TILE, rows, TILE), dtype=x.dtype, device=x.device)
     fn = getattr(_lib, f"rb_to_tiled_{_TORCH_SUFFIX[x.dtype]}")
-    _check(fn(x.data_ptr(), _ld(x), out.data_ptr(), rows, B, _stream_ptr(stream)), "to_tiled")
+    with torch.cuda.device(x.device):
+        _check(fn(x.data_ptr(), _ld(x), out.data_ptr(), rows, B, _stream_ptr(stream, x.device)), "to_tiled")
     return out
 
 
@@ -457,7 +516,8 @@ def from_tiled(t, B, stream=None):
     rows = t.shape[1]
     out = torch.empty((rows, B), dtype=t.dtype, device=t.device)
     fn = getattr(_lib, f"rb_from_tiled_{_TORCH_SUFFIX[t.dtype]}")
-    _check(fn(t.data_ptr(), out.data_ptr(), max(B, 1), rows, B, _stream_ptr(stream)), "from_tiled")
+    with torch.cuda.device(t.device):
+        _check(fn(t.data_ptr(), out.data_ptr(), max(B, 1), rows, B, _stream_ptr(stream, t.device)), "from_tiled")
     return out
 
 
@@ -471,6 +531,7 @@ def fill_uniform(t, lo, hi, seed, stream=None):
     if lo.shape != (rows,) or hi.shape != (rows,):
         raise ValueError("lo/hi must have one value per row")
     fn = getattr(_lib, f"rb_fill_uniform_{_TORCH_SUFFIX[t.dtype]}")
-    _check(fn(t.data_ptr(), rows, B, _ld(t), lo.ctypes.data_as(_dp), hi.ctypes.data_as(_dp),
-              ctypes.c_uint64(seed), _stream_ptr(stream)), "fill_uniform")
+    with torch.cuda.device(t.device):
+        _check(fn(t.data_ptr(), rows, B, _ld(t), lo.ctypes.data_as(_dp), hi.ctypes.data_as(_dp),
+                  ctypes.c_uint64(seed), _stream_ptr(stream, t.device)), "fill_uniform")
     return t

@@ -218,31 +218,72 @@ def test_set_tuning_rejects_unknown_key(ffi):
         ffi.set_tuning("no_such_knob", 1)
 
 
+def test_set_tuning_experimental_keys_gated(ffi):
+    """Only the production knobs (jit, pack, rnea_stream) are writable without
+    RB_EXPERIMENTAL=1; the A/B selectors are refused with a message naming the switch, and
+    the kernel forms measured and rejected in round 1 no longer exist at all."""
+    import os
+
+    if os.environ.get("RB_EXPERIMENTAL") == "1":
+        pytest.skip("experimental knobs enabled in this process")
+    for key in ("split_rot", "f64_tab", "jit_variant", "rnea_nt", "jit_waves", "opaque_consts"):
+        with pytest.raises(ffi.RigidBodyError, match="RB_EXPERIMENTAL"):
+            ffi.set_tuning(key, 0)
+    for key in ("rnea_seg", "rnea_tiles", "rnea_tile", "fd_stream"):
+        with pytest.raises(ffi.RigidBodyError, match="unknown tuning key"):
+            ffi.set_tuning(key, 1)
+    for key, dflt in (("jit", 1), ("pack", -1), ("rnea_stream", -1)):
+        ffi.set_tuning(key, dflt)
+
+
 def test_jit_kernel_forms_compile(ffi, fr3_text):
-    """Every model-specialised kernel form selectable by a tuning knob builds for gfx950
-    (hipRTC, no device) and its source carries the form: paired fp32 lanes (pack; FD default
-    for chains up to 8 links), table-assisted fp64 sincos (f64_tab, default on), segmented
-    RNEA (rnea_seg), multi-tile workgroups (rnea_tiles)."""
+    """Every model-specialised kernel form the production knobs select builds for gfx950
+    (hipRTC, no device) and its source carries the form: paired fp32 forward-dynamics lanes
+    (pack; default for chains up to 8 links) or one per lane, table-assisted fp64 sincos,
+    split joint rotation for signed-permutation frames."""
     from rigidbody_amd import chains
 
     mb = ffi.Multibody.from_urdf_string(fr3_text)
     c30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     assert "aba_lane2" in mb.jit_source(False, "fd")            # auto policy: paired FD
     assert "aba_lane2" not in c30.jit_source(False, "fd")       # ... not for 30 links
-    assert "rnea_lane2" not in mb.jit_source(False, "rnea")     # RNEA one per lane
+    assert "aba_lane2" not in mb.jit_source(True, "fd")         # ... nor fp64
+    assert "rnea_lane<" in mb.jit_source(False, "rnea")         # RNEA one per lane
     assert "sctab_init" in mb.jit_source(True, "rnea") and "sctab_init" not in mb.jit_source(False, "rnea")
-    forms = [("pack", 2, mb, "rnea", False, "rnea_lane2"), ("pack", 1, mb, "fd", False, "aba_lane<"),
-             ("f64_tab", 0, mb, "fd", True, "RB_SINCOS_TAB 0"), ("rnea_seg", 2, c30, "rnea", False, "rnea_lane_seg<T, N, 2"),
-             ("rnea_tiles", 4, mb, "rnea", True, "__launch_bounds__(1024)"),
-             ("split_rot", 0, mb, "crba", False, "RB_SPLIT_ROT 0")]
-    defaults = {"pack": -1, "f64_tab": -1, "rnea_seg": -1, "rnea_tiles": 1, "split_rot": -1}
     assert "RB_SPLIT_ROT 1" in mb.jit_source(False, "fd")  # FR3 frames are signed permutations
     try:
-        for key, val, m, kind, f64, marker in forms:
-            ffi.set_tuning(key, val)
-            assert marker in m.jit_source(f64, kind), (key, val)
-            assert m.jit_compile(f64=f64, kind=kind) > 1000, (key, val)
-            ffi.set_tuning(key, defaults[key])
+        for pack, marker in ((2, "aba_lane2"), (1, "aba_lane<")):
+            ffi.set_tuning("pack", pack)
+            assert marker in mb.jit_source(False, "fd"), pack
+            assert mb.jit_compile(f64=False, kind="fd") > 1000, pack
     finally:
-        for k, v in defaults.items():
-            ffi.set_tuning(k, v)
+        ffi.set_tuning("pack", -1)
+    for kind in ("rnea", "fd", "crba", "rollout"):
+        assert mb.jit_compile(f64=True, kind=kind) > 1000, kind
+
+
+def test_host_batch_shapes_checked(ffi):
+    """The host batch wrappers check every array is [n, B] before the library copies n*B
+    doubles from (and into) them: a short q would overflow the output, a short qd/tau be
+    over-read."""
+    mb = ffi.Multibody.new()
+    n, B = mb.n, 5
+    ok = np.zeros((n, B))
+    for bad in (np.zeros((n - 1, B)), np.zeros((n, B - 1)), np.zeros(n * B), np.zeros((n, B, 1))):
+        for args in ((bad, ok, ok), (ok, bad, ok), (ok, ok, bad)):
+            with pytest.raises(ValueError, match=r"\[7, B\]"):
+                mb.rnea_batch_host(*args)
+            with pytest.raises(ValueError, match=r"\[7, B\]"):
+                mb.fd_batch_host(*args)
+
+
+def test_one_device_per_call(ffi):
+    """Arrays of one batched call must share a device (the library launches on the current
+    device, which the wrappers set from the arrays); a mix is refused before any launch."""
+    import torch
+
+    from rigidbody_amd import ffi as mod
+
+    assert mod._one_device((torch.empty(1), torch.empty(2))) == torch.device("cpu")
+    with pytest.raises(ValueError, match="one device"):
+        mod._one_device((torch.empty(1), torch.empty(1, device="meta")))

@@ -237,17 +237,16 @@ def test_jit_and_generic_kernels_agree(name, ffi, dev, fr3_text):
     mb = ffi.Multibody.from_urdf_string(_model_xml(name, fr3_text))
     om = _oracle(_model_xml(name, fr3_text))
     try:
-        for jit, tile in ((1, 1), (1, 0), (0, 1)):
+        for jit in (1, 0):
             ffi.set_tuning("jit", jit)
-            ffi.set_tuning("rnea_tile", tile)
             for kind in ("rnea", "fd", "crba"):
                 for f64 in (False, True):
                     assert mb.kernel_path(kind, f64) == ("jit" if jit else "generic"), ffi.last_error()
             q, qd, qdd = (_t(g[k], dev) for k in ("q", "qd", "qdd"))
-            _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), g["tau"], 1e-9, f"rnea f64 jit={jit} tile={tile}")
+            _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), g["tau"], 1e-9, f"rnea f64 jit={jit}")
             q32, qd32, qdd32 = (x.float() for x in (q, qd, qdd))
             ref = om.rnea_batch(*[x.double().cpu().numpy() for x in (q32, qd32, qdd32)])
-            _close(mb.rnea_batch(q32, qd32, qdd32).cpu().numpy(), ref, 1e-4, f"rnea f32 jit={jit} tile={tile}")
+            _close(mb.rnea_batch(q32, qd32, qdd32).cpu().numpy(), ref, 1e-4, f"rnea f32 jit={jit}")
             tin = _t(g["tau_in"], dev)
             qdd_gpu = mb.fd_batch(q, qd, tin).cpu().numpy()
             res = om.rnea_batch(g["q"], g["qd"], qdd_gpu) - g["tau_in"]
@@ -255,12 +254,11 @@ def test_jit_and_generic_kernels_agree(name, ffi, dev, fr3_text):
             _close(mb.crba_batch(q).cpu().numpy(), g["H"], 1e-9, f"crba f64 jit={jit}")
     finally:
         ffi.set_tuning("jit", 1)
-        ffi.set_tuning("rnea_tile", 0)  # the library default (tuning.hpp)
 
 
-def test_tiled_kernel_partial_tiles_and_alignment(ffi, dev, fr3_text):
-    """The LDS-tiled JIT form: batches that end mid-tile, a misaligned leading dimension
-    (falls back to the per-lane form), and offset views all match the oracle."""
+def test_rnea_partial_blocks_and_alignment(ffi, dev, fr3_text):
+    """Batches that end mid-block, a leading dimension past the batch, and offset views
+    (a base pointer 1 element in) all match the oracle."""
     mb = ffi.Multibody.from_urdf_string(fr3_text)
     om = _oracle(fr3_text)
     rng = np.random.default_rng(11)
@@ -410,13 +408,13 @@ def test_single_config_abi_is_reentrant(dev):
     assert not errs, errs
 
 
-@pytest.mark.parametrize("kind", ["rnea", "fd"])
+@pytest.mark.parametrize("kind", ["fd"])
 def test_paired_lane_kernels(kind, ffi, dev, fr3_text):
-    """fp32 model-specialised kernels with two configurations per lane on packed fp32
-    (tuning `pack`, the default for chains up to 8 links) against the one-per-lane form and
-    the oracle: ragged batches (second configuration of a lane past B, an odd number of
-    256-configuration tiles), SoA and tiled.  rnea: 1e-4 * (1 + |tau|) against the fp64
-    oracle on the fp32-rounded inputs; fd: torque residual 1e-3 * (1 + |tau|)."""
+    """fp32 model-specialised forward dynamics with two configurations per lane on packed
+    fp32 (tuning `pack`, the default for chains up to 8 links at batches >= 2^18) against the
+    one-per-lane form and the oracle: ragged batches (second configuration of a lane past B,
+    an odd number of 256-configuration tiles), SoA and tiled; torque residual
+    1e-3 * (1 + |tau|) against the fp64 oracle on the fp32-rounded inputs."""
     mb = ffi.Multibody.from_urdf_string(fr3_text)
     om = _oracle(fr3_text)
     n = mb.n
@@ -450,95 +448,34 @@ def test_paired_lane_kernels(kind, ffi, dev, fr3_text):
             assert torch.equal(v, outs[(2, B, "soa" if lay == "tiled" else "tiled")][1])
 
 
-@pytest.mark.parametrize("seg", [2, 3, 5])
-def test_segmented_rnea_bit_identical(seg, ffi, dev, fr3_text):
-    """Segmented RNEA (tuning rnea_seg: the backward-sweep state held one segment at a time,
-    inputs reloaded per pass) runs exactly the one-pass operations: bit-identical outputs
-    for the 30- and 12-DOF chains and FR3, fp32 and fp64, SoA and tiled, ragged batches;
-    fp64 also against the oracle (1e-9)."""
-    from rigidbody_amd import chains
-
-    outs = {}
-    try:
-        for s in (0, seg):
-            ffi.set_tuning("rnea_seg", s)
-            for name, xml in (("chain30", chains.synthetic_chain_urdf(30)), ("chain12", chains.synthetic_chain_urdf(12)),
-                              ("fr3", fr3_text)):
-                mb = ffi.Multibody.from_urdf_string(xml)
-                n = mb.n
-                assert mb.kernel_path("rnea", False) == "jit"
-                for dt in (torch.float32, torch.float64):
-                    for B in (1, 300, 4096 + 5):
-                        rng = np.random.default_rng(B + n)
-                        x = [_t(rng.uniform(-2, 2, (n, B)), dev, dt) for _ in range(3)]
-                        outs[(s, name, dt, B, "soa")] = (xml, x, mb.rnea_batch(*x))
-                        xt = [ffi.to_tiled(a) for a in x]
-                        outs[(s, name, dt, B, "tiled")] = (xml, x, ffi.from_tiled(mb.rnea_batch_tiled(*xt, B), B))
-    finally:
-        ffi.set_tuning("rnea_seg", -1)
-    for (s, name, dt, B, lay), (xml, x, v) in outs.items():
-        if s == 0:
-            continue
-        ref = outs[(0, name, dt, B, lay)][2]
-        assert torch.equal(v, ref), (seg, name, dt, B, lay, (v - ref).abs().max().item())
-        if B == 300 and dt == torch.float64:  # fp32 one-pass accuracy: the golden tests
-            got = v.cpu().numpy()
-            want = _oracle(xml).rnea_batch(*[a.cpu().numpy() for a in x])
-            _close(got, want, 1e-9, f"seg={seg} {name}")
-
-
-@pytest.mark.parametrize("tiles", [2, 4])
-def test_rnea_workgroup_tiles_bit_identical(tiles, ffi, dev, fr3_text):
-    """JIT RNEA with 2 / 4 tiles of 256 configurations per workgroup (tuning rnea_tiles)
-    gives the 1-tile kernel's outputs bit for bit: ragged batches (partial last workgroup,
-    partial last tile), SoA and tiled, fp32 and fp64."""
+# ------------------------------------------------------- single-configuration dispatch
+def test_single_config_host_vs_gpu(ffi, dev, fr3_text):
+    """The single-configuration ABI on the host (default) and as a GPU launch
+    (rb_set_tuning("single_gpu", 1)) agree on the FR3 goldens, and the host lane bodies match
+    the precompiled GPU kernels (jit=0: the same code, the same packed constants) to within
+    a few ulp -- same formulation on both sides of the host/device split."""
+    g = load_npz("fr3_golden.npz")
     mb = ffi.Multibody.from_urdf_string(fr3_text)
-    outs = {}
+    assert mb.single_config_path() == "host"
+    host = [(mb.rnea(g["q"][:, b], g["qd"][:, b], g["qdd"][:, b]), mb.crba_raw(g["q"][:, b]),
+             mb.fwd_kin(g["q"][:, b]), mb.jac_raw(g["q"][:, b])) for b in range(32)]
     try:
-        for t in (1, tiles):
-            ffi.set_tuning("rnea_tiles", t)
-            for dt in (torch.float32, torch.float64):
-                for B in (1, 255, 257, 700, 1024, 4096 + 300):
-                    rng = np.random.default_rng(B)
-                    x = [_t(rng.uniform(-2, 2, (7, B)), dev, dt) for _ in range(3)]
-                    outs[(t, dt, B, "soa")] = mb.rnea_batch(*x)
-                    xt = [ffi.to_tiled(a) for a in x]
-                    outs[(t, dt, B, "tiled")] = ffi.from_tiled(mb.rnea_batch_tiled(*xt, B), B)
+        ffi.set_tuning("single_gpu", 1)
+        assert mb.single_config_path() == "gpu"
+        for b in range(32):
+            gpu = (mb.rnea(g["q"][:, b], g["qd"][:, b], g["qdd"][:, b]), mb.crba_raw(g["q"][:, b]),
+                   mb.fwd_kin(g["q"][:, b]), mb.jac_raw(g["q"][:, b]))
+            for h, d in zip(host[b], gpu):
+                assert np.abs(h - d).max() <= 1e-12 * (1 + np.abs(d).max()), b
     finally:
-        ffi.set_tuning("rnea_tiles", 1)
-    for (t, dt, B, lay), v in outs.items():
-        if t != 1:
-            assert torch.equal(v, outs[(1, dt, B, lay)]), (tiles, dt, B, lay)
-
-
-@pytest.mark.parametrize("knob", ["fd_stream", "rnea_stream"])
-def test_resident_grid_stride_forms(knob, ffi, dev, fr3_text):
-    """The resident grid-stride JIT forms (A/B knobs fd_stream / rnea_stream: a resident-sized
-    grid walking the batch with a register prefetch of the next block) meet the oracle
-    tolerances on ragged batches that take several passes per block: fp64 1e-9 (rnea tau; fd
-    through the torque residual 1e-8), fp32 1e-4 (rnea) / residual 1e-3 (fd); SoA, and tiled
-    for fd (the tiled RNEA launch uses the lane kernel)."""
-    mb = ffi.Multibody.from_urdf_string(fr3_text)
-    om = _oracle(fr3_text)
-    kind = "fd" if knob == "fd_stream" else "rnea"
+        ffi.set_tuning("single_gpu", 0)
     try:
-        ffi.set_tuning(knob, 1)
-        for dt, tol in ((torch.float64, 1e-9), (torch.float32, 1e-4)):
-            for B in (1, 257, 3 * 65536 + 5, (1 << 20) + 77):
-                rng = np.random.default_rng(B)
-                x = [_t(rng.uniform(-2, 2, (7, B)), dev, dt) for _ in range(3)]
-                outs = {"soa": (mb.rnea_batch if kind == "rnea" else mb.fd_batch)(*x)}
-                if kind == "fd":
-                    outs["tiled"] = ffi.from_tiled(mb.fd_batch_tiled(*[ffi.to_tiled(a) for a in x], B), B)
-                cols = np.unique(np.r_[np.arange(min(B, 300)), np.arange(max(0, B - 300), B)])
-                xs = [a.double().cpu().numpy()[:, cols] for a in x]
-                for lay, v in outs.items():
-                    got = v.double().cpu().numpy()[:, cols]
-                    if kind == "rnea":
-                        _close(got, om.rnea_batch(*xs), tol, f"{knob} {dt} B={B} {lay}")
-                    else:
-                        res = om.rnea_batch(xs[0], xs[1], got) - xs[2]
-                        lim = 1e-8 if dt == torch.float64 else 1e-3
-                        assert (np.abs(res) / (1 + np.abs(xs[2]))).max() <= lim, (knob, dt, B, lay)
+        ffi.set_tuning("jit", 0)
+        q, qd, qdd = (_t(g[k][:, :32], dev) for k in ("q", "qd", "qdd"))
+        tau = mb.rnea_batch(q, qd, qdd).cpu().numpy()
+        H = mb.crba_batch(q).cpu().numpy()
     finally:
-        ffi.set_tuning(knob, 0 if knob == "fd_stream" else -1)
+        ffi.set_tuning("jit", 1)
+    for b in range(32):
+        assert np.abs(host[b][0] - tau[:, b]).max() <= 1e-14 * (1 + np.abs(tau[:, b]).max()), b
+        assert np.abs(host[b][1] - H[:, b]).max() <= 1e-14 * (1 + np.abs(H[:, b]).max()), b

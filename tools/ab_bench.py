@@ -14,6 +14,8 @@ import sys
 import numpy as np
 import torch
 
+os.environ.setdefault("RB_EXPERIMENTAL", "1")  # A/B selectors (tuning.hpp) are experimental keys
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "rigidbody-rs_amd")]
 import bench  # noqa: E402
@@ -50,9 +52,8 @@ def main():
     lib = ffi.lib()
     # every knob any variant sets is reset to the library default (tuning.hpp) before each
     # variant, so a knob of one variant never leaks into the next
-    defaults = {"rnea_stream": -1, "grid_factor": 1, "jit": 1, "rnea_tile": 0, "rnea_nt": 3, "fd_nt": 3,
-                "jit_waves": -1, "opaque_consts": -1, "fd_stream": 0, "pack": -1, "f64_tab": -1, "rnea_seg": -1,
-                "rnea_tiles": 1, "split_rot": -1, "jit_variant": 0}
+    defaults = {"rnea_stream": -1, "grid_factor": 1, "jit": 1, "rnea_nt": 3, "fd_nt": 3, "jit_waves": -1,
+                "opaque_consts": -1, "pack": -1, "f64_tab": -1, "split_rot": -1, "jit_variant": 0}
     used = {kv.split("=")[0] for v in a.variants for kv in v.split(",")} - {"streams"}
     keys = [(v, lp) for v in a.variants for lp in launches]
     res = {k: [] for k in keys}
