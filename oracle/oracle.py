@@ -13,13 +13,16 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# ORACLE_LIB: an alternative build of the same source (the ASan/UBSan one, `make sanitize`)
+_LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 _dp = ctypes.POINTER(ctypes.c_double)
 
 
 def build(force: bool = False) -> str:
+    if os.environ.get("ORACLE_LIB"):
+        return _LIB_PATH
     if force or not os.path.exists(_LIB_PATH) or (
         os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "oracle.c"))
     ):

@@ -2,6 +2,7 @@
 #include "urdf.hpp"
 
 #include <cctype>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -22,9 +23,14 @@ const XmlNode *XmlNode::child(const char *t) const {
 
 namespace {
 
+// Nesting limit: element() recurses per level, so an adversarial document of deeply nested
+// tags would otherwise exhaust the stack (URDFs nest 4-5 levels).
+constexpr int kMaxDepth = 256;
+
 struct Parser {
     const std::string &s;
     size_t i = 0;
+    int depth = 0;
 
     [[noreturn]] void fail(const char *what) const {
         throw std::runtime_error(std::string("XML parse error at offset ") + std::to_string(i) +
@@ -80,13 +86,14 @@ struct Parser {
     }
     XmlNode element() {
         if (i >= s.size() || s[i] != '<') fail("expected '<'");
+        if (++depth > kMaxDepth) fail("elements nested too deeply");
         ++i;
         XmlNode n;
         n.tag = name();
         for (;;) {
             skip_ws();
             if (i >= s.size()) fail("unterminated start tag");
-            if (starts("/>")) { i += 2; return n; }
+            if (starts("/>")) { i += 2; --depth; return n; }
             if (s[i] == '>') { ++i; break; }
             std::string k = name();
             skip_ws();
@@ -110,6 +117,7 @@ struct Parser {
                 skip_ws();
                 if (i >= s.size() || s[i] != '>') fail("expected '>'");
                 ++i;
+                --depth;
                 return n;
             }
             n.children.push_back(element());
@@ -124,6 +132,7 @@ void parse_numbers(const char *text, double *out, int n, const char *what) {
         char *end = nullptr;
         double v = std::strtod(p, &end);
         if (end == p) throw std::runtime_error(std::string("bad number list in ") + what);
+        if (!std::isfinite(v)) throw std::runtime_error(std::string("non-finite number in ") + what);
         out[k] = v;
         p = end;
     }

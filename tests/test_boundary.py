@@ -287,3 +287,61 @@ def test_one_device_per_call(ffi):
     assert mod._one_device((torch.empty(1), torch.empty(2))) == torch.device("cpu")
     with pytest.raises(ValueError, match="one device"):
         mod._one_device((torch.empty(1), torch.empty(1, device="meta")))
+
+
+@pytest.mark.parametrize("xml,needle", [
+    ("", "XML parse error"),
+    ("<robot", "XML parse error"),
+    ("<robot name='r'><!-- never closed", "XML parse error"),
+    ("<robot name=r></robot>", "XML parse error"),
+    ("<robot name='r'></robott>", "mismatched closing tag"),
+    ("<robot name='r\x00'><link/></robot>", "no non-fixed joint"),
+    ("<" * 5000 + "robot>", "XML parse error"),
+    ("<a>" * 100000, "nested too deeply"),
+    ("<robot><link name='a'><inertial><mass value='nan'/></inertial></link></robot>", "non-finite"),
+    ("<robot><link name='a'><inertial><mass value='1e999'/></inertial></link></robot>", "non-finite"),
+    ("<robot><link name='a'><inertial><mass value='abc'/></inertial></link></robot>", "bad number"),
+    ("<robot><link name='a'><inertial><origin xyz='1 2'/></inertial></link></robot>", "bad number list"),
+    ("<robot><link name='a'><inertial><origin xyz='1 2 3 4'/></inertial></link></robot>", "too many numbers"),
+    ("<robot><link name='a'/><joint name='j' type='revolute'><origin rpy='0 0 inf'/>"
+     "<parent link='a'/><child link='a'/></joint></robot>", "non-finite"),
+])
+def test_malformed_urdf_rejected(ffi, xml, needle):
+    """Malformed / adversarial URDF text is refused with a message (never a crash): truncation,
+    unterminated comments, unquoted attributes, mismatched tags, NUL bytes, deep nesting
+    (the parser recurses per level: capped at 256), non-finite or missing numbers.  The
+    sanitized build (`make -C rigidbody-rs_amd sanitize`) runs these under ASan/UBSan."""
+    with pytest.raises(ffi.RigidBodyError, match=needle):
+        ffi.Multibody.from_urdf_string(xml)
+
+
+def test_mutated_fr3_never_crashes(ffi, fr3_text):
+    """600 deterministic mutants of the FR3 URDF (truncations, byte flips, deleted or inserted
+    markup characters, duplicated spans): each either loads a model or raises with a message."""
+    rng = np.random.default_rng(20250224)
+    text = fr3_text.encode()
+    loaded = refused = 0
+    for k in range(600):
+        b = bytearray(text)
+        op = k % 5
+        at = int(rng.integers(0, len(b)))
+        if op == 0:
+            b = b[:at]
+        elif op == 1:
+            b[at] = int(rng.integers(1, 256))
+        elif op == 2:
+            del b[at:at + int(rng.integers(1, 40))]
+        elif op == 3:
+            b[at:at] = bytes([ord(c) for c in rng.choice(list("<>/='\" &;"), 3)])
+        else:
+            n = int(rng.integers(1, 400))
+            b[at:at] = b[at:at + n]
+        xml = b.decode("latin-1")
+        try:
+            mb = ffi.Multibody.from_urdf_string(xml)
+            assert mb.n >= 1
+            loaded += 1
+        except ffi.RigidBodyError as e:
+            assert str(e)
+            refused += 1
+    assert loaded + refused == 600 and refused > 100

@@ -9,6 +9,8 @@
 3. Physics invariants (SURVEY.md §8(c) ii-vi).
 4. The committed golden vectors (tests/golden, tools/gen_golden.py) still reproduce.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -193,15 +195,26 @@ def test_reference_asset_matches_compact(fr3_text):
 
 
 # ------------------------------------------------------ 4. golden vectors
+def _same_as_golden(a, b):
+    """The committed goldens came from the gcc build of oracle.c, which reproduces them bit for
+    bit; the clang ASan/UBSan build (ORACLE_LIB, `make sanitize`) rounds a few results 1 ulp
+    apart, amplified by the 30-DOF chain's cond(H) ~ 1e5 in its forward dynamics, so it is held
+    to 1e-10 of the array's scale instead."""
+    if os.environ.get("ORACLE_LIB"):
+        assert np.abs(np.asarray(a) - b).max() <= 1e-10 * (1 + np.abs(b).max())
+    else:
+        np.testing.assert_array_equal(a, b)
+
+
 def test_golden_main_cpp(fr3_text, oracle_mod):
     _, m, _ = _models(fr3_text)
     g = load_json("main_cpp_case.json")
     for c in g["cases"].values():
         q, dq, ddq = (np.array(c[k], float) for k in ("q", "dq", "ddq"))
-        np.testing.assert_array_equal(m.rnea(q, dq, ddq), c["tau"])
-        np.testing.assert_array_equal(m.crba_raw(q), c["crba_raw"])
-        np.testing.assert_array_equal(m.fwd_kin(q), c["fwd_kin"])
-        np.testing.assert_array_equal(m.jac_raw(q), c["jac_raw"])
+        _same_as_golden(m.rnea(q, dq, ddq), c["tau"])
+        _same_as_golden(m.crba_raw(q), c["crba_raw"])
+        _same_as_golden(m.fwd_kin(q), c["fwd_kin"])
+        _same_as_golden(m.jac_raw(q), c["jac_raw"])
 
 
 @pytest.mark.parametrize("name", ["fr3_golden.npz", "chain12_golden.npz", "chain30_golden.npz"])
@@ -219,6 +232,7 @@ def test_golden_sets(name, fr3_text, oracle_mod):
         lo, hi = chains.input_ranges(lim, kind)
         key = "tau_in" if kind == "tau" else kind
         np.testing.assert_array_equal(chains.host_uniform(raw["n"], g["q"].shape[1], lo, hi, seed + k), g[key])
-    np.testing.assert_array_equal(m.rnea_batch(g["q"], g["qd"], g["qdd"], nthreads=2), g["tau"])
-    np.testing.assert_array_equal(m.fd_batch(g["q"], g["qd"], g["tau_in"], nthreads=2), g["qdd_fd"])
-    np.testing.assert_array_equal(m.crba_batch(g["q"], nthreads=2), g["H"])
+    same = _same_as_golden
+    same(m.rnea_batch(g["q"], g["qd"], g["qdd"], nthreads=2), g["tau"])
+    same(m.fd_batch(g["q"], g["qd"], g["tau_in"], nthreads=2), g["qdd_fd"])
+    same(m.crba_batch(g["q"], nthreads=2), g["H"])
