@@ -63,6 +63,24 @@ def _close(got, ref, rel, what):
     return err.max()
 
 
+# fp32 forward dynamics, backward-error bound (SURVEY §8(c) "qdd ... reported against
+# cond(H)"): an fp32 solve is backward stable -- qdd32 solves (H + dH) qdd = tau - C(q, qd)
+# with |dH| ~ k eps32 |H| -- so its torque residual r = rnea64(q, qd, qdd32) - tau obeys
+#   |r_i| <= K * eps32 * (1 + |tau_i| + (|H_sym| |qdd32|)_i)
+# independently of cond(H), where the forward error |qdd32 - qdd| grows with cond(H).
+FD32_BACKWARD_K = 16.0  # measured 2.6 on the 30-DOF chain at 2^20 (4096 spot columns)
+
+
+def fp32_fd_backward_ratio(res, Hraw, qdd32, tau):
+    """K needed per element: |r| / (eps32 (1 + |tau| + |H_sym| |qdd32|)); Hraw [n*n, B]
+    column-major upper triangle (the CRBA output), res / qdd32 / tau [n, B]."""
+    n, B = tau.shape
+    Hu = np.abs(Hraw).reshape(n, n, B).transpose(1, 0, 2)  # [row, col, b]
+    Ha = np.triu(Hu.transpose(2, 0, 1)) + np.triu(Hu.transpose(2, 0, 1), 1).transpose(0, 2, 1)  # [b, r, c]
+    scale = 1 + np.abs(tau) + np.einsum("brc,cb->rb", Ha, np.abs(qdd32))
+    return np.abs(res) / (float(np.finfo(np.float32).eps) * scale)
+
+
 # ------------------------------------------------------------ single-config ABI
 def test_single_config_abi_main_cpp(ffi, dev, fr3_text):
     """multibody_rnea/crba/fwd_kin/jac (lib.rs:15-70) on the main.cpp input, fp64 on GPU."""
@@ -121,13 +139,16 @@ def test_batched_f32_vs_golden(name, ffi, dev, fr3_text):
     _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), tau_ref, 1e-4, "rnea f32")
     qdd32 = mb.fd_batch(q, qd, tin).cpu().numpy().astype(np.float64)
     res = om.rnea_batch(q64, qd64, qdd32) - t64
-    if name.startswith("chain30"):
-        assert (np.abs(res).max(axis=0) / (1 + np.abs(t64).max(axis=0))).max() <= 1e-2
-    else:
-        assert (np.abs(res) / (1 + np.abs(t64))).max() <= 1e-3
     qdd_ref = om.fd_batch(q64, qd64, t64)
     Hb = om.crba_batch(q64)
     n = q64.shape[0]
+    # SURVEY §8(c)'s element-wise 1e-3 torque residual is out of reach in fp32 for the 30-DOF
+    # chain (cond(H) ~ 1e5: an fp32 emulation of the same algorithm already leaves 4.9e-3), so
+    # every model is held to the backward-error form (fp32_fd_backward_ratio), the others to
+    # the element-wise 1e-3 as well.
+    if not name.startswith("chain30"):
+        assert (np.abs(res) / (1 + np.abs(t64))).max() <= 1e-3
+    assert fp32_fd_backward_ratio(res, Hb, qdd32, t64).max() <= FD32_BACKWARD_K
     eps32 = float(np.finfo(np.float32).eps)
     for b in range(q64.shape[1]):
         Hm = Hb[:, b].reshape(n, n).T
@@ -189,6 +210,70 @@ def test_device_fill_matches_host(ffi, dev):
 
 
 # ------------------------------------------------------------ full size (2^20)
+def test_chain30_full_size_f32(ffi, dev):
+    """SURVEY §8(d) config 5 at its bench size: the synthetic 30-DOF chain, B = 2^20, fp32.
+    All 2^20 columns: fp32 RNEA against the fp64 RNEA kernel on the same fp32-rounded inputs,
+    column-norm-wise max_i |dtau_i| <= 1e-4 (1 + max_i |tau_i|) (measured 1.3e-5; the fp64
+    kernel is pinned to the oracle at 1e-9 below).  SURVEY §8(c)'s element-wise 1e-4 holds for
+    FR3 at this size (1.1e-5) but not in this chain's tail: a root torque of ~0.1 Nm left over
+    from ~3000 Nm link terms loses its digits to cancellation in ANY fp32 evaluation (7e-4 with
+    the precise sincos too, tools/diag_c30.py), so the 30-link bound is norm-wise.  The fp64
+    fd -> rnea round trip (1e-8 scaled) and rnea affine in qdd with slope H (fp64, 1e-9); fp32
+    forward dynamics through the backward-error bound; oracle spot columns (fp32 1e-4, fp64
+    1e-9).  Reference: multibody.rs:111-174."""
+    from rigidbody_amd import chains
+
+    xml = chains.synthetic_chain_urdf(30)
+    mb = ffi.Multibody.from_urdf_string(xml)
+    om = _oracle(xml)
+    n, B = 30, 1 << 20
+    lim = mb.limits()
+    x = {}
+    for k, kind in enumerate(("q", "qd", "qdd", "tau")):
+        lo, hi = chains.input_ranges(lim, kind)
+        t = ffi.fill_uniform(torch.empty((n, B), dtype=torch.float32, device=dev), lo, hi, chains.SEED + k)
+        x[kind] = t
+    x64 = {k: v.double() for k, v in x.items()}  # the fp32-rounded inputs in fp64
+    tau32 = mb.rnea_batch(x["q"], x["qd"], x["qdd"])
+    tau64 = mb.rnea_batch(x64["q"], x64["qd"], x64["qdd"])
+    dtau = (tau32.double() - tau64).abs()
+    rel = (dtau.max(0).values / (1 + tau64.abs().max(0).values)).max().item()
+    assert rel <= 1e-4, rel
+    ew = (dtau / (1 + tau64.abs())).max().item()  # element-wise, reported
+    del tau32, dtau
+    # fp64 round trip and affine-in-qdd on every column, in chunks (H is 900 values per column)
+    C = 1 << 17
+    worst_rt = worst_aff = 0.0
+    for c0 in range(0, B, C):
+        sl = slice(c0, c0 + C)
+        q, qd, qdd, tau = (x64[k][:, sl].contiguous() for k in ("q", "qd", "qdd", "tau"))
+        back = mb.rnea_batch(q, qd, mb.fd_batch(q, qd, tau))
+        worst_rt = max(worst_rt, ((back - tau).abs() / (1 + tau.abs())).max().item())
+        d = tau64[:, sl] - mb.rnea_batch(q, qd, torch.zeros_like(q))
+        Hf = mb.crba_batch(q).reshape(n, n, C).permute(2, 1, 0)  # [b, row, col]
+        Hs = torch.triu(Hf) + torch.triu(Hf, 1).transpose(1, 2)
+        hq = torch.einsum("brc,cb->rb", Hs, qdd)
+        worst_aff = max(worst_aff, ((d - hq).abs() / (1 + d.abs() + hq.abs())).max().item())
+        del Hf, Hs, hq, d, back
+    assert worst_rt <= 1e-8, worst_rt
+    assert worst_aff <= 1e-9, worst_aff
+    # fp32 forward dynamics: backward-error bound on spot columns (needs |H| per column)
+    idx = torch.linspace(0, B - 1, 4096, device=dev).long()
+    qdd32 = mb.fd_batch(x["q"], x["qd"], x["tau"])[:, idx].double().cpu().numpy()
+    xs = {k: x64[k][:, idx].cpu().numpy() for k in x64}
+    res = om.rnea_batch(xs["q"], xs["qd"], qdd32) - xs["tau"]
+    K = fp32_fd_backward_ratio(res, om.crba_batch(xs["q"]), qdd32, xs["tau"]).max()
+    assert K <= FD32_BACKWARD_K, K
+    # oracle spot columns
+    ref = om.rnea_batch(xs["q"], xs["qd"], xs["qdd"])
+    _close(tau64[:, idx].cpu().numpy(), ref, 1e-9, "chain30 2^20 spot f64")
+    sub = [x[k][:, idx].contiguous() for k in ("q", "qd", "qdd")]
+    got = mb.rnea_batch(*sub).double().cpu().numpy()
+    assert (np.abs(got - ref).max(0) / (1 + np.abs(ref).max(0))).max() <= 1e-4
+    print(f"chain30 2^20: f32-vs-f64 norm-wise {rel:.2e} (element-wise {ew:.2e}), round trip {worst_rt:.2e}, "
+          f"affine {worst_aff:.2e}, fd32 backward K {K:.1f}")
+
+
 def test_full_size_properties(ffi, dev, fr3_text):
     """BASELINE config size (fr3, B = 2^20): the oracle cannot cover every column, so
     check size-independent properties on all of them plus an oracle spot check:
