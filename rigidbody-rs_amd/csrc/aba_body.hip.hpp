@@ -159,26 +159,26 @@ __device__ __forceinline__ void aba_lane(const T *mdl, const T *__restrict__ q, 
 }
 
 // Paired lane (fp32 model-specialised kernels, spatial.hip.hpp f2): the configurations at
-// lane offset `off` of the batch blocks starting at elements oA and oB; loads in the same
-// first-use order as aba_lane.
+// byte offsets offA / offB from the pair's base (ld_row2); loads in the same first-use order
+// as aba_lane.
 template <int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void aba_lane2(const f2 *mdl, const float *__restrict__ q, const float *__restrict__ qd,
-                                          const float *__restrict__ tau, float *__restrict__ qdd, int64_t oA,
-                                          int64_t oB, uint32_t off, int64_t ld) {
+                                          const float *__restrict__ tau, float *__restrict__ qdd, uint32_t offA,
+                                          uint32_t offB, int64_t ld) {
     f2 qv[N], qdv[N], tv[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        qv[j] = ld_row2(q, oA, oB, j * ld, off);
+        qv[j] = ld_row2(q, j * ld, offA, offB);
         __builtin_amdgcn_sched_barrier(0);
-        qdv[j] = ld_row2(qd, oA, oB, j * ld, off);
+        qdv[j] = ld_row2(qd, j * ld, offA, offB);
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int j = N - 1; j >= 0; --j) {
-        tv[j] = ld_row2(tau, oA, oB, j * ld, off);
+        tv[j] = ld_row2(tau, j * ld, offA, offB);
         __builtin_amdgcn_sched_barrier(0);
     }
-    aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 v) { st_row2(qdd, oA, oB, j * ld, off, v); });
+    aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
 }
 
 // Fused rollout (the MPC-shooting use of forward dynamics): K steps

@@ -156,7 +156,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         "  const uint32_t bA = blockIdx.x * 512u + threadIdx.x;\n"
         "  if (bA >= B) return;\n"
         "  const int64_t oA = (int64_t)(2u * blockIdx.x) * bs;\n"
-        "  const int64_t oB = bA + 256u < B ? oA + bs : oA;\n";
+        "  const uint32_t offA = threadIdx.x * 4u;\n"
+        "  const uint32_t offB = bA + 256u < B ? offA + (uint32_t)bs * 4u : offA;\n";
     std::string head_s = "extern \"C\" __global__ __launch_bounds__(256) ";
     if (const int w = jit_waves(kind, f64, m.n))
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
@@ -177,7 +178,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         if (pack == 2) {
             o << pair_prologue;
             o << "  rbamd::dev::aba_lane2<N, " << F
-              << ", Topo>(kModel, q, qd, tau, qdd, oA, oB, threadIdx.x * 4u, ld);\n}\n";
+              << ", Topo>(kModel, q + oA, qd + oA, tau + oA, qdd + oA, offA, offB, ld);\n}\n";
         } else {
             o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
             o << "  if (b >= B) return;\n";

@@ -430,17 +430,17 @@ __device__ __forceinline__ double recip(double x) {
 }
 __device__ __forceinline__ f2 recip(f2 x) { return f2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; }
 
-// Paired-lane row access: one configuration from each of two batch blocks (base offsets oA,
-// oB in elements, the same lane byte offset), so each half's loads/stores stay fully
-// coalesced dword rows in either layout.
-__device__ __forceinline__ f2 ld_row2(const float *__restrict__ base, int64_t oA, int64_t oB, int64_t row,
-                                      uint32_t off) {
-    return f2{ld_row(base + oA, row, off), ld_row(base + oB, row, off)};
+// Paired-lane row access: one configuration from each of two batch blocks.  Both halves
+// use the saddr form off ONE wave-uniform base (the pair's first block, element oA): the
+// first at the lane's byte offset offA, the second at offB = offA + the block stride in bytes
+// (or offA itself when the second configuration is past B) -- per-lane 32-bit offsets, no
+// 64-bit address arithmetic per row (a per-lane second base cost 2 v_lshl_add_u64 per row).
+__device__ __forceinline__ f2 ld_row2(const float *__restrict__ base, int64_t row, uint32_t offA, uint32_t offB) {
+    return f2{ld_row(base, row, offA), ld_row(base, row, offB)};
 }
-__device__ __forceinline__ void st_row2(float *__restrict__ base, int64_t oA, int64_t oB, int64_t row, uint32_t off,
-                                        f2 v) {
-    st_row(base + oA, row, off, v.x);
-    st_row(base + oB, row, off, v.y);
+__device__ __forceinline__ void st_row2(float *__restrict__ base, int64_t row, uint32_t offA, uint32_t offB, f2 v) {
+    st_row(base, row, offA, v.x);
+    st_row(base, row, offB, v.y);
 }
 
 }  // namespace dev
