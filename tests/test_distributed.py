@@ -41,8 +41,28 @@ WORKER = textwrap.dedent('''
     mx = rdist.max_over_ranks([float(rank + 1), 10.0 - rank], world, dev)
     tot = rdist.sum_over_ranks([1.0], world, dev)
     sl = [rdist.shard(1 << 20, r, world) for r in range(world)]
+    # dynamics per rank: the strong split of one global batch of 96 configurations, each rank
+    # evaluating its shard through the single-configuration ABI (host lane bodies, no GPU here),
+    # gathered to rank 0 and checked there against the oracle on the whole batch
+    G = 96
+    xs = [chains.host_uniform(mb.n, G, *chains.input_ranges(lim, k), chains.SEED + i)
+          for i, k in enumerate(("q", "qd", "qdd"))]
+    b0, b1 = rdist.shard(G, rank, world)
+    mine = np.stack([mb.rnea(xs[0][:, b], xs[1][:, b], xs[2][:, b]) for b in range(b0, b1)], axis=1)
+    parts = [None] * world
+    dist.all_gather_object(parts, (b0, b1, mine.tolist()))
+    err = None
     if rank == 0:
-        print(json.dumps({{"sums": sums, "max": mx, "tot": tot, "shards": sl, "n": mb.n}}))
+        from oracle import oracle, urdf_model
+        om = oracle.Model(urdf_model.model_raw_from_urdf(chains.synthetic_chain_urdf(12)))
+        tau = np.zeros((mb.n, G))
+        for p0, p1, v in parts:
+            tau[:, p0:p1] = np.asarray(v)
+        ref = om.rnea_batch(*xs)
+        err = float((np.abs(tau - ref) / (1 + np.abs(ref))).max())
+    if rank == 0:
+        print(json.dumps({{"sums": sums, "max": mx, "tot": tot, "shards": sl, "n": mb.n, "rnea_err": err,
+                          "covered": sorted((p[0], p[1]) for p in parts)}}))
     dist.destroy_process_group()
 ''')
 
@@ -71,6 +91,9 @@ def test_gloo_model_broadcast_and_sharding(world, tmp_path):
     sl = res["shards"]
     assert sl[0][0] == 0 and sl[-1][1] == 1 << 20
     assert all(sl[i][1] == sl[i + 1][0] for i in range(world - 1))
+    cov = res["covered"]  # the ranks' shards of the 96-configuration batch tile it exactly
+    assert cov[0][0] == 0 and cov[-1][1] == 96 and all(cov[i][1] == cov[i + 1][0] for i in range(world - 1))
+    assert res["rnea_err"] <= 1e-12, res["rnea_err"]
 
 
 def test_shard_ranges_cover_exactly():
