@@ -358,7 +358,7 @@ def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED):
 
 
 def measure(mb, kernel, dt_name, B, layout, steps, warmup, world, rotate_gib, seed, spinup_ms=300.0, streams=1,
-            sync_every=0, graph=False):
+            sync_every=0, graph=False, extra_streams=()):
     """Time `steps` launches of `kernel` over batches of B resident configurations.
     Returns a dict (wall, kernel_ms_avg, bytes, sets) plus the graph-replay figures if asked."""
     ds = DT[dt_name]
@@ -371,6 +371,8 @@ def measure(mb, kernel, dt_name, B, layout, steps, warmup, world, rotate_gib, se
     if graph:
         gw, gkm, gl = time_graph(launch, steps)
         r.update({"graph_wall": gw, "graph_kernel_ms_avg": gkm, "graph_launches": gl})
+    if extra_streams:
+        r["streams_ms"] = {ns: time_launches(launch, steps, warmup, world, 50.0, ns)[1] for ns in extra_streams}
     del sets, launch
     torch.cuda.empty_cache()
     return r
@@ -381,8 +383,9 @@ def side_workloads(mb7, a):
     sec = {}
     steps = max(20, a.steps // 4)
 
-    def one(name, mb, kernel, dt_name, B=a.batch, layout=a.layout, graph=False):
-        r = measure(mb, kernel, dt_name, B, layout, steps, 5, 1, a.rotate_gib, chains.SEED + 31, graph=graph)
+    def one(name, mb, kernel, dt_name, B=a.batch, layout=a.layout, graph=False, streams=(1,)):
+        r = measure(mb, kernel, dt_name, B, layout, steps, 5, 1, a.rotate_gib, chains.SEED + 31, graph=graph,
+                    extra_streams=streams[1:])
         sec[name] = {"evals_per_s": B * steps / r["wall"], "kernel_ms_avg": r["kernel_ms_avg"], "batch": B,
                      "layout": layout, "dtype": dt_name, "hbm_frac": r["bytes"] / (r["kernel_ms_avg"] * 1e-3) / HBM_PEAK,
                      "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64") for k in kernel.split("_"))}
@@ -393,11 +396,16 @@ def side_workloads(mb7, a):
                                     "dtype": dt_name, "launches": gl,
                                     "hbm_frac": r["bytes"] / (r["graph_kernel_ms_avg"] * 1e-3) / HBM_PEAK,
                                     "launch": "HIP graph of 100 captured C-ABI launches, replayed"}
+        for ns, km in r.get("streams_ms", {}).items():  # independent batches kept in flight on ns streams
+            sec[f"{name}_{ns}streams"] = {"evals_per_s": B / (km * 1e-3), "step_ms_device": km, "batch": B,
+                                          "dtype": dt_name, "streams": ns,
+                                          "hbm_frac_effective": r["bytes"] / (km * 1e-3) / HBM_PEAK,
+                                          "launch": f"consecutive batches rotate over {ns} HIP streams"}
 
-    one("rnea_fr3_f32_b65536", mb7, "rnea", "f32", 65536, graph=True)    # config 2
-    one("fd_fr3_f32_b65536", mb7, "fd", "f32", 65536, graph=True)        # config 3
+    one("rnea_fr3_f32_b65536", mb7, "rnea", "f32", 65536, graph=True, streams=(1, 2, 4))    # config 2
+    one("fd_fr3_f32_b65536", mb7, "fd", "f32", 65536, graph=True, streams=(1, 2, 4))        # config 3
     one("fd_fr3_f64", mb7, "fd", "f64")
-    one("fd_fr3_f32", mb7, "fd", "f32")
+    one("fd_fr3_f32", mb7, "fd", "f32", streams=(1, 2))
     one("rnea_fd_fr3_f64_b131072", mb7, "rnea_fd", "f64", 1 << 17, graph=True)  # config 4, one GPU's 2^17 shard
     mb30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     mb30.upload()

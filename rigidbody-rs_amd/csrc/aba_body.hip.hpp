@@ -181,6 +181,33 @@ __device__ __forceinline__ void aba_lane2(const f2 *mdl, const float *__restrict
     aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
 }
 
+// Sequential pair (tuning pack=3, A/B): the configurations at byte offsets offA and offB
+// (the second only when `two`) evaluated one after the other from one load burst, so the
+// second's rows land while the first computes.
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
+__device__ __forceinline__ void aba_lane_seq2(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                              const T *__restrict__ tau, T *__restrict__ qdd, uint32_t offA,
+                                              uint32_t offB, bool two, int64_t ld) {
+    T qa[N], qda[N], ta[N], qb[N], qdb[N], tb[N];
+    const uint32_t ob = two ? offB : offA;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qa[j] = ld_row(q, j * ld, offA);
+        qda[j] = ld_row(qd, j * ld, offA);
+    }
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) ta[j] = ld_row(tau, j * ld, offA);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qb[j] = ld_row(q, j * ld, ob);
+        qdb[j] = ld_row(qd, j * ld, ob);
+    }
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) tb[j] = ld_row(tau, j * ld, ob);
+    aba_any<T, N, FAST, Topo>(mdl, qa, qda, ta, [&](int j, T v) { st_row(qdd, j * ld, offA, v); });
+    if (two) aba_any<T, N, FAST, Topo>(mdl, qb, qdb, tb, [&](int j, T v) { st_row(qdd, j * ld, offB, v); });
+}
+
 // Fused rollout (the MPC-shooting use of forward dynamics): K steps
 // of semi-implicit Euler, qd += dt * fd(q, qd, tau_k); q += dt * qd.  q, qd [n][ld] are
 // read once and overwritten with the final state; tau_seq is [K][n][ld]; traj

@@ -168,8 +168,14 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     return it->second.function ? &it->second : nullptr;
 }
 
-const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast) {
-    return jit_get(mb, rbamd::JitKind::Rnea, f64, fast);
+// Smallest batch for which the auto policy takes the sequential-pair fp64 RNEA (jit_pack 3):
+// it halves the waves, so below two resident rounds of the one-per-lane kernel (4 waves/SIMD x
+// 1024 SIMDs x 64 lanes x 2) the one-per-lane kernel keeps more of the chip busy.
+constexpr uint32_t kSeqMinBatch = 1u << 19;
+
+const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast, uint32_t B) {
+    const int pack = (rbamd::tuning().pack < 0 && B < kSeqMinBatch) ? 1 : 0;
+    return jit_get(mb, rbamd::JitKind::Rnea, f64, fast, pack);
 }
 
 // A tree / prismatic model has no precompiled kernel: without its hipRTC kernel the launch
@@ -192,7 +198,7 @@ hipError_t no_generic(const Multibody *mb) {
 constexpr uint32_t kPackMinBatch = 1u << 18;
 
 hipError_t jit_launch(const rbamd::JitKernel *jk, uint32_t B, void **args, hipStream_t s) {
-    const unsigned per_block = 256u * (unsigned)jk->pack;
+    const unsigned per_block = 256u * (jk->pack >= 2 ? 2u : 1u);
     const unsigned g = (unsigned)(((uint64_t)B + per_block - 1) / per_block);
     return hipModuleLaunchKernel(jk->function, g, 1, 1, 256u, 1, 1, 0, s, args, nullptr);
 }
@@ -204,7 +210,7 @@ template <typename T>
 hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *qdd, T *tau,
                            uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig())) {
+    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig(), B)) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&lda, (void *)&bs};
         return jit_launch(jk, B, args, s);

@@ -61,16 +61,21 @@ int jit_waves(JitKind kind, bool f64, int n) {
 }
 
 int jit_pack(JitKind kind, bool f64, int n) {
-    // Only fp32 forward dynamics pairs.  The rollout is not paired: with its K loop around the
-    // dynamics the pair needs 256 VGPRs (1 wave/SIMD) unpinned, or spills at 2-4 waves with
-    // pinned constants.  The RNEA pair (128 VGPRs, 4 waves/SIMD instead of 8) measured slower,
-    // 22.6 vs 21.0 us, although it issues half the VALU work, and was removed.
-    if (f64 || kind != JitKind::Fd) return 1;
+    // 2 = two configurations per lane on packed fp32 (fp32 forward dynamics of chains up to 8
+    // links: FR3 2^20 tiled 28.7 vs 30.7 us; 200+ VGPRs for the pair, 2 waves/SIMD; the
+    // 30-link chain needs ~240 VGPRs for one configuration).  The RNEA pair (128 VGPRs, 4
+    // waves/SIMD instead of 8) measured slower, 22.6 vs 21.0 us, and was removed; the rollout is
+    // not paired (256 VGPRs unpinned with its K loop, spills pinned).
+    // 3 = two configurations per lane evaluated one after the other from one load burst (the
+    // fp64 RNEA of chains up to 8 links: 125 VGPRs, still 4 waves/SIMD; FR3 2^20 tiled
+    // 42.0-42.8 us steady where the one-per-lane kernel alternates between ~40.7 and ~48.8 us
+    // phases, mean 44.3-44.6).
+    if (kind != JitKind::Fd && kind != JitKind::Rnea) return 1;
     const int v = tuning().pack;
-    if (v >= 0) return v >= 2 ? 2 : 1;
-    // Auto: chains up to 8 links (FR3 fp32 2^20 tiled: 28.7 vs 30.7 us; 200 VGPRs for the
-    // pair, 2 waves/SIMD).  The 30-link chain needs ~240 VGPRs for one configuration.
-    return n <= 8 ? 2 : 1;
+    if (v == 3) return 3;
+    if (v >= 0) return (v >= 2 && !f64 && kind == JitKind::Fd) ? 2 : 1;
+    if (kind == JitKind::Rnea) return (f64 && n <= 8) ? 3 : 1;
+    return (!f64 && n <= 8) ? 2 : 1;
 }
 
 bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
@@ -158,6 +163,15 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         "  const int64_t oA = (int64_t)(2u * blockIdx.x) * bs;\n"
         "  const uint32_t offA = threadIdx.x * 4u;\n"
         "  const uint32_t offB = bA + 256u < B ? offA + (uint32_t)bs * 4u : offA;\n";
+    // Sequential pair (pack 3): lane t of batch blocks 2k and 2k+1, evaluated one after the
+    // other from one load burst; the second only when it exists (twoB).
+    const std::string seq_prologue =
+        "  const uint32_t bA = blockIdx.x * 512u + threadIdx.x;\n"
+        "  if (bA >= B) return;\n"
+        "  const int64_t oA = (int64_t)(2u * blockIdx.x) * bs;\n"
+        "  const uint32_t offA = threadIdx.x * (uint32_t)sizeof(T);\n"
+        "  const bool twoB = bA + 256u < B;\n"
+        "  const uint32_t offB = offA + (uint32_t)bs * (uint32_t)sizeof(T);\n";
     std::string head_s = "extern \"C\" __global__ __launch_bounds__(256) ";
     if (const int w = jit_waves(kind, f64, m.n))
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
@@ -165,7 +179,13 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     const char *head = head_s.c_str();
     // Lane kernels take the block stride bs (elements): 256 for SoA, N * 256 for the tiled
     // layout (kernels.hpp); block k's arrays start at element k * bs, lane offset threadIdx.x.
-    if (kind == JitKind::Rnea) {
+    if (kind == JitKind::Rnea && pack == 3) {
+        o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+             "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
+        o << seq_prologue;
+        o << "  rbamd::dev::rnea_lane_seq2<T, N, " << F
+          << ", Topo>(kModel, q + oA, qd + oA, qdd + oA, tau + oA, offA, offB, twoB, ld);\n}\n";
+    } else if (kind == JitKind::Rnea) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
@@ -175,7 +195,11 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
-        if (pack == 2) {
+        if (pack == 3) {
+            o << seq_prologue;
+            o << "  rbamd::dev::aba_lane_seq2<T, N, " << F
+              << ", Topo>(kModel, q + oA, qd + oA, tau + oA, qdd + oA, offA, offB, twoB, ld);\n}\n";
+        } else if (pack == 2) {
             o << pair_prologue;
             o << "  rbamd::dev::aba_lane2<N, " << F
               << ", Topo>(kModel, q + oA, qd + oA, tau + oA, qdd + oA, offA, offB, ld);\n}\n";

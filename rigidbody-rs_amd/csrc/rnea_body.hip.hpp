@@ -134,6 +134,19 @@ __device__ __forceinline__ void rnea_lane(const T *mdl, const T *__restrict__ q,
     rnea_any<T, N, FAST, Topo>(mdl, qv, qdv, qddv, [&](int j, T v) { st_row(tau, j * ld, off, v); });
 }
 
+// Sequential pair (tuning pack=3, A/B): see aba_lane_seq2.
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
+__device__ __forceinline__ void rnea_lane_seq2(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                               const T *__restrict__ qdd, T *__restrict__ tau, uint32_t offA,
+                                               uint32_t offB, bool two, int64_t ld) {
+    T qa[N], qda[N], qdda[N], qb[N], qdb[N], qddb[N];
+    const uint32_t ob = two ? offB : offA;
+    load_cfg<T, N>(q, qd, qdd, ld, offA, qa, qda, qdda);
+    load_cfg<T, N>(q, qd, qdd, ld, ob, qb, qdb, qddb);
+    rnea_any<T, N, FAST, Topo>(mdl, qa, qda, qdda, [&](int j, T v) { st_row(tau, j * ld, offA, v); });
+    if (two) rnea_any<T, N, FAST, Topo>(mdl, qb, qdb, qddb, [&](int j, T v) { st_row(tau, j * ld, offB, v); });
+}
+
 // Streaming form (precompiled generic kernels, rnea.hip): walk the batch with `stride`,
 // prefetching the next configuration's joint values into registers before evaluating the
 // current one.

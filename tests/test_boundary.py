@@ -248,14 +248,18 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "aba_lane2" in mb.jit_source(False, "fd")            # auto policy: paired FD
     assert "aba_lane2" not in c30.jit_source(False, "fd")       # ... not for 30 links
     assert "aba_lane2" not in mb.jit_source(True, "fd")         # ... nor fp64
-    assert "rnea_lane<" in mb.jit_source(False, "rnea")         # RNEA one per lane
+    assert "rnea_lane<" in mb.jit_source(False, "rnea")         # fp32 RNEA one per lane
+    assert "rnea_lane_seq2<" in mb.jit_source(True, "rnea")     # fp64 RNEA: sequential pair
+    assert "rnea_lane<" in c30.jit_source(True, "rnea")         # ... up to 8 links
     assert "sctab_init" in mb.jit_source(True, "rnea") and "sctab_init" not in mb.jit_source(False, "rnea")
     assert "RB_SPLIT_ROT 1" in mb.jit_source(False, "fd")  # FR3 frames are signed permutations
     try:
-        for pack, marker in ((2, "aba_lane2"), (1, "aba_lane<")):
+        for pack, marker in ((2, "aba_lane2"), (1, "aba_lane<"), (3, "aba_lane_seq2<")):
             ffi.set_tuning("pack", pack)
             assert marker in mb.jit_source(False, "fd"), pack
             assert mb.jit_compile(f64=False, kind="fd") > 1000, pack
+        ffi.set_tuning("pack", 1)
+        assert "rnea_lane<" in mb.jit_source(True, "rnea")
     finally:
         ffi.set_tuning("pack", -1)
     for kind in ("rnea", "fd", "crba", "rollout"):

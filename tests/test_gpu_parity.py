@@ -564,3 +564,38 @@ def test_single_config_host_vs_gpu(ffi, dev, fr3_text):
     for b in range(32):
         assert np.abs(host[b][0] - tau[:, b]).max() <= 1e-14 * (1 + np.abs(tau[:, b]).max()), b
         assert np.abs(host[b][1] - H[:, b]).max() <= 1e-14 * (1 + np.abs(H[:, b]).max()), b
+
+
+@pytest.mark.parametrize("kind", ["rnea", "fd"])
+def test_sequential_pair_bit_identical(kind, ffi, dev, fr3_text):
+    """Two configurations per lane evaluated one after the other (tuning pack=3: lane t of
+    batch blocks 2k and 2k+1 from one load burst) runs exactly the one-per-lane operations:
+    bit-identical outputs, fp32 and fp64, SoA and tiled, ragged batches (a lane whose second
+    configuration is past B, an odd number of blocks); fp64 also against the oracle."""
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    om = _oracle(fr3_text)
+    outs = {}
+    try:
+        for pack in (1, 3):
+            ffi.set_tuning("pack", pack)
+            for dt in (torch.float32, torch.float64):
+                for B in (1, 255, 257, 511, 513, 767, 65536 + 3):
+                    rng = np.random.default_rng(B)
+                    x = [_t(rng.uniform(-2, 2, (7, B)), dev, dt) for _ in range(3)]
+                    f = mb.rnea_batch if kind == "rnea" else mb.fd_batch
+                    ft = mb.rnea_batch_tiled if kind == "rnea" else mb.fd_batch_tiled
+                    outs[(pack, dt, B, "soa")] = (x, f(*x))
+                    outs[(pack, dt, B, "tiled")] = (x, ffi.from_tiled(ft(*[ffi.to_tiled(a) for a in x], B), B))
+    finally:
+        ffi.set_tuning("pack", -1)
+    for (pack, dt, B, lay), (x, v) in outs.items():
+        if pack != 3:
+            continue
+        assert torch.equal(v, outs[(1, dt, B, lay)][1]), (kind, dt, B, lay)
+        if dt == torch.float64 and B in (257, 767):
+            xs = [a.cpu().numpy() for a in x]
+            if kind == "rnea":
+                _close(v.cpu().numpy(), om.rnea_batch(*xs), 1e-9, f"seq2 rnea B={B} {lay}")
+            else:
+                res = om.rnea_batch(xs[0], xs[1], v.cpu().numpy()) - xs[2]
+                assert (np.abs(res) / (1 + np.abs(xs[2]))).max() <= 1e-8, (B, lay)

@@ -4,7 +4,8 @@ thousand launches over rotated buffers, timed per chunk of 100 launches (one hip
 per chunk).  Separates clock/power behaviour of the memory system (both drift) from
 behaviour tied to the kernel's own VALU load (only RNEA drifts).
 
-usage: python tools/drift.py [launches_per_phase]
+usage: python tools/drift.py [launches_per_phase] [--dtype f32|f64] [--packs -1 3 ...]
+  --packs: RNEA under each rb_set_tuning("pack", v) in alternation instead of RNEA vs probe
 """
 import ctypes
 import json
@@ -34,14 +35,36 @@ def series(launch, n, chunk=100):
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 4000
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("n", nargs="?", type=int, default=4000)
+    ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--packs", nargs="*", type=int, default=None)
+    a = ap.parse_args()
+    n = a.n
     B = 1 << 20
+    dt = bench.DT[a.dtype]
     mb = ffi.Multibody.new()
     mb.upload()
-    per = bench.set_bytes(7, B, 4, "rnea")
+    per = bench.set_bytes(7, B, 4 if a.dtype == "f32" else 8, "rnea")
     nsets = max(2, int(np.ceil(1.25 * (1 << 30) / per)))
-    sets = bench.make_sets(mb, B, torch.float32, "rnea", nsets, 20250224, layout="tiled")
-    rl = bench.batch_launcher(mb, sets, "rnea", torch.float32, "tiled", B)
+    sets = bench.make_sets(mb, B, dt, "rnea", nsets, 20250224, layout="tiled")
+    rl = bench.batch_launcher(mb, sets, "rnea", dt, "tiled", B)
+    if a.packs:
+        res = {}
+        for rep in range(2):
+            for pk in a.packs:
+                ffi.set_tuning("pack", pk)
+                rl(0, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                torch.cuda.synchronize()
+                s = series(lambda k: rl(k, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), n)
+                name = f"pack={pk}#{rep}"
+                res[name] = {"us_mean": float(np.mean(s)), "us_min": min(s), "us_max": max(s),
+                             "us_p10": float(np.percentile(s, 10)), "us_p90": float(np.percentile(s, 90))}
+                print(name, json.dumps(res[name]), flush=True)
+        ffi.set_tuning("pack", -1)
+        return
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     lib = ffi.lib()
     pin = [(torch.rand((21, B), device="cuda"), torch.empty((7, B), device="cuda")) for _ in range(nsets)]
