@@ -41,6 +41,7 @@ def main():
     ap.add_argument("n", nargs="?", type=int, default=4000)
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--packs", nargs="*", type=int, default=None)
+    ap.add_argument("--reps", type=int, default=2)
     a = ap.parse_args()
     n = a.n
     B = 1 << 20
@@ -53,7 +54,7 @@ def main():
     rl = bench.batch_launcher(mb, sets, "rnea", dt, "tiled", B)
     if a.packs:
         res = {}
-        for rep in range(2):
+        for rep in range(a.reps):
             for pk in a.packs:
                 ffi.set_tuning("pack", pk)
                 rl(0, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
