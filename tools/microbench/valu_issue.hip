@@ -41,7 +41,7 @@ __global__ __launch_bounds__(64) void chain_kernel(float *out, long long *cyc, i
 }
 
 template <int MODE, int CHAINS>
-void run(const char *name, int grid, float *dout, long long *dcyc, int half) {
+void run(const char *name, int grid, float *dout, long long *dcyc, int half, int waves_per_simd = 1) {
     hipLaunchKernelGGL((chain_kernel<MODE, CHAINS>), dim3(grid), dim3(64), 0, 0, dout, dcyc, half, 1.0f);
     hipDeviceSynchronize();
     hipLaunchKernelGGL((chain_kernel<MODE, CHAINS>), dim3(grid), dim3(64), 0, 0, dout, dcyc, half, 1.0f);
@@ -51,7 +51,8 @@ void run(const char *name, int grid, float *dout, long long *dcyc, int half) {
     double sum = 0;
     for (auto x : c) sum += (double)x;
     const double per = sum / grid / ((double)kIters * CHAINS);
-    printf("{\"op\": \"%s\", \"chains\": %d, \"half_exec\": %d, \"cycles_per_instr\": %.3f}\n", name, CHAINS, half, per);
+    printf("{\"op\": \"%s\", \"chains\": %d, \"half_exec\": %d, \"waves_per_simd\": %d, \"cycles_per_instr_per_wave\": %.3f, \"simd_cycles_per_instr\": %.3f}\n",
+           name, CHAINS, half, waves_per_simd, per, per / waves_per_simd);
 }
 
 int main() {
@@ -61,8 +62,15 @@ int main() {
     const int grid = 4 * cus;
     float *dout;
     long long *dcyc;
-    hipMalloc(&dout, grid * 64 * sizeof(float));
-    hipMalloc(&dcyc, grid * sizeof(long long));
+    hipMalloc(&dout, 8 * grid * 64 * sizeof(float));
+    hipMalloc(&dcyc, 8 * grid * sizeof(long long));
+    // several waves per SIMD: the grid holds k waves per SIMD, all resident at once (tiny kernels)
+    for (int k : {2, 4, 8}) {
+        run<0, 8>("v_fma_f32", k * grid, dout, dcyc, 0, k);
+        run<1, 8>("v_pk_fma_f32", k * grid, dout, dcyc, 0, k);
+        run<0, 1>("v_fma_f32", k * grid, dout, dcyc, 0, k);
+        run<1, 1>("v_pk_fma_f32", k * grid, dout, dcyc, 0, k);
+    }
     for (int half = 0; half < 2; ++half) {
         run<0, 1>("v_fma_f32", grid, dout, dcyc, half);
         run<0, 8>("v_fma_f32", grid, dout, dcyc, half);
