@@ -198,7 +198,7 @@ hipError_t no_generic(const Multibody *mb) {
 constexpr uint32_t kPackMinBatch = 1u << 18;
 
 hipError_t jit_launch(const rbamd::JitKernel *jk, uint32_t B, void **args, hipStream_t s) {
-    const unsigned per_block = 256u * (jk->pack >= 2 ? 2u : 1u);
+    const unsigned per_block = 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
     const unsigned g = (unsigned)(((uint64_t)B + per_block - 1) / per_block);
     return hipModuleLaunchKernel(jk->function, g, 1, 1, 256u, 1, 1, 0, s, args, nullptr);
 }

@@ -263,6 +263,21 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     code->resize(code_size);
     hiprtcGetCode(prog, code->data());
     hiprtcDestroyProgram(&prog);
+    // RB_JIT_DUMP=dir: keep every compiled source and code object for inspection
+    // (llvm-objdump / llvm-readelf on the .co: registers, scratch, ISA of what really runs)
+    if (const char *dir = std::getenv("RB_JIT_DUMP")) {
+        static int seq = 0;
+        const std::string base = std::string(dir) + "/jit_" + std::to_string(seq++) + "_k" +
+                                 std::to_string((int)kind) + (f64 ? "_f64" : "_f32") + "_p" + std::to_string(pack);
+        if (FILE *f = std::fopen((base + ".hip").c_str(), "wb")) {
+            std::fwrite(src.data(), 1, src.size(), f);
+            std::fclose(f);
+        }
+        if (FILE *f = std::fopen((base + ".co").c_str(), "wb")) {
+            std::fwrite(code->data(), 1, code->size(), f);
+            std::fclose(f);
+        }
+    }
     return true;
 }
 
