@@ -9,6 +9,7 @@
 // caller asks for the GPU (tuning single_gpu).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -80,9 +81,18 @@ struct Multibody {
     std::vector<double> pk64;
     mutable std::mutex mu;
     mutable std::map<int, DeviceConsts> dev;
-    // model-specialised hipRTC kernels, keyed by (device, dtype, fast trig, stream form)
+    // model-specialised hipRTC kernels, keyed by (device, kind, dtype, trig, tuning tag, form)
     mutable std::map<std::string, rbamd::JitKernel> jit;
     mutable std::map<std::string, int> jit_device;
+    // per-launch fast path of jit_get: [device][kind][f64][fast trig][requested pack] -> the
+    // kernel resolved under tuning generation `gen` (map nodes never move or die before free)
+    struct JitSlot {
+        std::atomic<unsigned> gen{0};
+        std::atomic<const rbamd::JitKernel *> jk{nullptr};
+    };
+    mutable JitSlot jit_fast[16][6][2][2][4];
+    // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
+    mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
 
 namespace {
@@ -117,6 +127,13 @@ int device_consts(const Multibody *mb, const T **out) {
     int d = 0;
     hipError_t e = hipGetDevice(&d);
     if (e != hipSuccess) return hip_err(e, "hipGetDevice");
+    std::atomic<const void *> *fastp = (d >= 0 && d < 16) ? &mb->dc_fast[d][sizeof(T) == 8 ? 1 : 0] : nullptr;
+    if (fastp) {
+        if (const void *p = fastp->load(std::memory_order_acquire)) {
+            *out = static_cast<const T *>(p);
+            return RB_OK;
+        }
+    }
     std::lock_guard<std::mutex> lk(mb->mu);
     DeviceConsts &dc = mb->dev[d];
     if constexpr (sizeof(T) == 4) {
@@ -131,6 +148,7 @@ int device_consts(const Multibody *mb, const T **out) {
             dc.f32 = static_cast<float *>(p);
         }
         *out = reinterpret_cast<const T *>(dc.f32);
+        if (fastp) fastp->store(dc.f32, std::memory_order_release);
     } else {
         if (!dc.f64) {
             void *p = nullptr;
@@ -143,6 +161,7 @@ int device_consts(const Multibody *mb, const T **out) {
             dc.f64 = static_cast<double *>(p);
         }
         *out = reinterpret_cast<const T *>(dc.f64);
+        if (fastp) fastp->store(dc.f64, std::memory_order_release);
     }
     return RB_OK;
 }
@@ -155,6 +174,12 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
     const bool fst = fast && !f64;
+    const unsigned gen = rbamd::tuning_generation();
+    Multibody::JitSlot *slot = nullptr;
+    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 4) {
+        slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack];
+        if (slot->gen.load(std::memory_order_acquire) == gen) return slot->jk.load(std::memory_order_relaxed);
+    }
     if (pack <= 0) pack = rbamd::jit_pack(kind, f64, mb->model.n);
     const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
                             (fst ? ":fast" : ":precise") + rbamd::jit_tag(kind, f64, mb->model.n) + ":q" +
@@ -165,7 +190,12 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
         it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, pack)).first;
         mb->jit_device[key] = d;
     }
-    return it->second.function ? &it->second : nullptr;
+    const rbamd::JitKernel *res = it->second.function ? &it->second : nullptr;
+    if (slot) {
+        slot->jk.store(res, std::memory_order_relaxed);
+        slot->gen.store(gen, std::memory_order_release);
+    }
+    return res;
 }
 
 // Smallest batch for which the auto policy takes the sequential-pair fp64 RNEA (jit_pack 3):
@@ -197,10 +227,13 @@ hipError_t no_generic(const Multibody *mb) {
 // of it (2 blocks of 512 configurations per CU x 256 CUs) -- 2^18.
 constexpr uint32_t kPackMinBatch = 1u << 18;
 
-hipError_t jit_launch(const rbamd::JitKernel *jk, uint32_t B, void **args, hipStream_t s) {
+unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
     const unsigned per_block = 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
-    const unsigned g = (unsigned)(((uint64_t)B + per_block - 1) / per_block);
-    return hipModuleLaunchKernel(jk->function, g, 1, 1, 256u, 1, 1, 0, s, args, nullptr);
+    return (unsigned)(((uint64_t)B + per_block - 1) / per_block);
+}
+
+hipError_t jit_launch(const rbamd::JitKernel *jk, uint32_t B, void **args, hipStream_t s) {
+    return hipModuleLaunchKernel(jk->function, jit_grid(jk, B), 1, 1, 256u, 1, 1, 0, s, args, nullptr);
 }
 
 // tiled: the [ceil(B/256)][n][256] layout (kernels.hpp); the JIT lane kernels and the
@@ -577,7 +610,6 @@ double *multibody_crba(const Multibody *mb, const double *q) {
 
 double *multibody_fwd_kin(const Multibody *mb, const double *q) {
     const double *in[1] = {q};
-    const size_t n = mb ? (size_t)mb->model.n : 0;
     bool host = false;
     double *r = single_host(mb, in, 1, 3, &host, [&](double *o) {
         return rbamd::host_fwd_kin(mb->model, mb->pk64.data(), q, o);

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -65,11 +66,18 @@ Tuning &tuning() {
     return t;
 }
 
+namespace {
+std::atomic<unsigned> g_generation{1};
+}
+
+unsigned tuning_generation() { return g_generation.load(std::memory_order_acquire); }
+
 int tuning_set(const char *key, int value) {
     for (const Key &k : kKeys) {
         if (std::strcmp(k.name, key) != 0) continue;
         if (k.experimental && !tuning_experimental()) return 2;
         tuning().*(k.field) = value;
+        g_generation.fetch_add(1, std::memory_order_acq_rel);
         return 0;
     }
     return 1;

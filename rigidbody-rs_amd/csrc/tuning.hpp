@@ -63,6 +63,10 @@ bool tuning_experimental();
 // Sets `key`; returns 0, 1 (unknown key) or 2 (experimental key without RB_EXPERIMENTAL=1).
 int tuning_set(const char *key, int value);
 
+// Bumped by every successful tuning_set (>= 1): per-launch caches keyed on the tuning state
+// (capi.cpp jit_get's fast path) compare it instead of rebuilding their string keys.
+unsigned tuning_generation();
+
 // Blocks for a streaming launch of `kfn`: factor x (resident blocks per CU x CUs) on the
 // current device, never more than `full` (one block per 256 configurations).  Cached per
 // (device, kernel).
