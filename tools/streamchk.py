@@ -1,5 +1,6 @@
-"""A/B parity of a forward-dynamics kernel form (jit_variant V, RB_EXPERIMENTAL) against the
-default form and the fp64 kernel, SoA and tiled, at 2^20 and ragged sizes.  usage: streamchk.py [V]"""
+"""A/B parity of a kernel form (jit_variant V, RB_EXPERIMENTAL) against the default form and
+the fp64 kernel, SoA and tiled, fp32 and fp64, at 2^20 and ragged sizes.
+usage: streamchk.py [V] [fd|rnea]"""
 import os, sys
 os.environ["RB_EXPERIMENTAL"]="1"
 sys.path[:0]=[os.getcwd(), os.path.join(os.getcwd(),"rigidbody-rs_amd")]
@@ -7,19 +8,26 @@ import torch
 from rigidbody_amd import ffi
 mb=ffi.Multibody.new(); mb.upload()
 V=int(sys.argv[1]) if len(sys.argv)>1 else 128
+K=sys.argv[2] if len(sys.argv)>2 else "fd"
+soa_fn=getattr(mb, K+"_batch"); til_fn=getattr(mb, K+"_batch_tiled")
 ok=True
 for B in (1<<20, 65536, 1000, 777, 70001, 513, 256):
     g=torch.Generator(device="cuda").manual_seed(B)
     q=torch.rand((7,B),device="cuda",generator=g)*6-3; qd=torch.rand((7,B),device="cuda",generator=g)*4-2; tau=torch.rand((7,B),device="cuda",generator=g)*20-10
-    ref=mb.fd_batch(q.double(),qd.double(),tau.double())
-    tq,tqd,tt=(ffi.to_tiled(x) for x in (q,qd,tau))
-    outs=[];touts=[]
-    for v in (0,V):
-        ffi.set_tuning("jit_variant",v)
-        outs.append(mb.fd_batch(q,qd,tau).clone())
-        touts.append(ffi.from_tiled(mb.fd_batch_tiled(tq,tqd,tt,B),B).clone())
+    ffi.set_tuning("jit_variant",0)
+    ref=soa_fn(q.double(),qd.double(),tau.double())
+    res={}
+    for dt in (torch.float32, torch.float64):
+        a,b_,c=(x.to(dt) for x in (q,qd,tau))
+        tq,tqd,tt=(ffi.to_tiled(x) for x in (a,b_,c))
+        outs=[];touts=[]
+        for v in (0,V):
+            ffi.set_tuning("jit_variant",v)
+            outs.append(soa_fn(a,b_,c).clone())
+            touts.append(ffi.from_tiled(til_fn(tq,tqd,tt,B),B).clone())
+        res[f"soa_{str(dt)[-7:]}"]=outs; res[f"tiled_{str(dt)[-7:]}"]=touts
     torch.cuda.synchronize()
-    for nm,o in (("soa",outs),("tiled",touts)):
+    for nm,o in res.items():
         same=torch.equal(o[0],o[1])
         e=[((x.double()-ref).norm(dim=0)/(1+ref.norm(dim=0))).max().item() for x in o]
         nd=(o[0]!=o[1]).sum().item()
