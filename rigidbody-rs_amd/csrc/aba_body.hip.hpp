@@ -297,5 +297,52 @@ __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T 
     }
 }
 
+// Paired rollout (fp32 model-specialised kernels, pack 2): the configurations at byte offsets
+// offA / offB of the SoA rows (spatial.hip.hpp f2 lanes, as aba_lane2), both states in LDS
+// between steps as f2 pairs, row-strided by the block.
+template <int N>
+struct RolloutShared2 {
+    f2 x[2 * N * kRolloutBlock];
+};
+
+template <int N, bool FAST, typename Topo = SerialTopo>
+__device__ __forceinline__ void rollout_lane2(const f2 *mdl, float *__restrict__ q, float *__restrict__ qd,
+                                              const float *__restrict__ tau_seq, float dt, int K,
+                                              float *__restrict__ traj, uint32_t offA, uint32_t offB, int64_t ld,
+                                              RolloutShared2<N> &sh) {
+    f2 *sx = sh.x + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        sx[j * kRolloutBlock] = ld_row2(q, j * ld, offA, offB);
+        sx[(N + j) * kRolloutBlock] = ld_row2(qd, j * ld, offA, offB);
+    }
+    const f2 dt2 = f2{dt, dt};
+    for (int k = 0; k < K; ++k) {
+        // row offsets re-derived per step (scalar ALU): hoisted out of the K loop they would
+        // hold 2N 64-bit values in SGPRs, spilled to VGPRs, across every step
+        int64_t ldk = ld;
+        asm volatile("" : "+s"(ldk));
+        f2 qv[N], qdv[N], tv[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = sx[j * kRolloutBlock];
+            qdv[j] = sx[(N + j) * kRolloutBlock];
+            tv[j] = ld_row2(tau_seq, ((int64_t)k * N + j) * ldk, offA, offB);
+        }
+        aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 a) {
+            const f2 qdn = fmadd(dt2, a, sx[(N + j) * kRolloutBlock]);
+            const f2 qn = fmadd(dt2, qdn, sx[j * kRolloutBlock]);
+            sx[(N + j) * kRolloutBlock] = qdn;
+            sx[j * kRolloutBlock] = qn;
+            if (traj) st_row2(traj, ((int64_t)k * N + j) * ldk, offA, offB, qn);
+        });
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        st_row2(q, j * ld, offA, offB, sx[j * kRolloutBlock]);
+        st_row2(qd, j * ld, offA, offB, sx[(N + j) * kRolloutBlock]);
+    }
+}
+
 }  // namespace dev
 }  // namespace rbamd

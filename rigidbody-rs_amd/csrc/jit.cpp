@@ -57,21 +57,25 @@ bool jit_opaque(JitKind kind, bool f64, int n) {
 int jit_waves(JitKind kind, bool f64, int n) {
     const int v = tuning().jit_waves;
     if (v >= 0) return v;
-    return (kind == JitKind::Rollout && !f64 && n <= 8) ? 4 : 0;
+    if (kind == JitKind::Rollout && !f64 && n <= 8) return jit_pack(kind, f64, n) == 2 ? 2 : 4;
+    return 0;
 }
 
 int jit_pack(JitKind kind, bool f64, int n) {
     // 2 = two configurations per lane on packed fp32 (fp32 forward dynamics of chains up to 8
     // links: FR3 2^20 tiled 28.7 vs 30.7 us; 200+ VGPRs for the pair, 2 waves/SIMD; the
     // 30-link chain needs ~240 VGPRs for one configuration).  The RNEA pair (128 VGPRs, 4
-    // waves/SIMD instead of 8) measured slower, 22.6 vs 21.0 us, and was removed; the rollout is
-    // not paired (256 VGPRs unpinned with its K loop, spills pinned).
+    // waves/SIMD instead of 8) measured slower, 22.6 vs 21.0 us, and was removed.  The fp32
+    // rollout of chains up to 8 links is paired too (rollout_lane2: 251 VGPRs, 2 waves/SIMD,
+    // constants pinned in SGPRs and machine LICM off so the K loop hoists nothing; FR3 2^20
+    // x 16 steps 317-323 vs 333-335 us one per lane at 4 waves/SIMD).
     // 3 = two configurations per lane evaluated one after the other from one load burst (the
     // fp64 RNEA of chains up to 8 links: 125 VGPRs, still 4 waves/SIMD; FR3 2^20 tiled
     // 42.0-42.8 us steady where the one-per-lane kernel alternates between ~40.7 and ~48.8 us
     // phases, mean 44.3-44.6).
-    if (kind != JitKind::Fd && kind != JitKind::Rnea) return 1;
     const int v = tuning().pack;
+    if (kind == JitKind::Rollout) return ((v < 0 || v == 2) && !f64 && n <= 8) ? 2 : 1;
+    if (kind != JitKind::Fd && kind != JitKind::Rnea) return 1;
     if (v == 3) return 3;
     if (v >= 0) return (v >= 2 && !f64 && kind == JitKind::Fd) ? 2 : 1;
     if (kind == JitKind::Rnea) return (f64 && n <= 8) ? 3 : 1;
@@ -209,6 +213,14 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
             o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
             o << "  rbamd::dev::aba_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
         }
+    } else if (kind == JitKind::Rollout && pack == 2) {
+        o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
+             "int K, T *__restrict__ traj, uint32_t B, int64_t ld) {\n";
+        o << "  __shared__ rbamd::dev::RolloutShared2<N> sh;\n";
+        o << "  const uint32_t bA = blockIdx.x * 512u + threadIdx.x;\n";
+        o << "  if (bA >= B) return;\n";
+        o << "  const uint32_t offA = bA * 4u, offB = bA + 256u < B ? offA + 1024u : offA;\n";
+        o << "  rbamd::dev::rollout_lane2<N, " << F << ", Topo>(kModel, q, qd, tau_seq, dt, K, traj, offA, offB, ld, sh);\n}\n";
     } else if (kind == JitKind::Rollout) {
         o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
              "int K, T *__restrict__ traj, uint32_t B, int64_t ld) {\n";
@@ -248,7 +260,14 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     }
     const std::string arch_opt = "--offload-arch=" + arch;
     const char *opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffinite-math-only", "-fno-signed-zeros"};
-    hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
+    std::vector<const char *> optv(opts, opts + sizeof(opts) / sizeof(opts[0]));
+    // The paired rollout keeps 2 waves/SIMD only without machine LICM: hoisting per-step
+    // address arithmetic out of its K loop costs the last VGPRs below 256.
+    if (kind == JitKind::Rollout && (pack > 0 ? pack : jit_pack(kind, f64, m.n)) == 2) {
+        optv.push_back("-mllvm");
+        optv.push_back("-disable-machine-licm");
+    }
+    hiprtcResult rc = hiprtcCompileProgram(prog, (int)optv.size(), optv.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);

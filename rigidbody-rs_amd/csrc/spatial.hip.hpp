@@ -202,7 +202,18 @@ RB_HD T mconst(T v) {
     }
     return v;
 }
-RB_HD f2 mconst(f2 v) { return v; }  // paired kernels do not pin constants
+RB_HD f2 mconst(f2 v) {
+    // Paired kernels pin only under a runtime loop (the paired rollout): one SGPR per
+    // constant, which v_pk_fma broadcasts to both halves.
+    if constexpr (RB_OPAQUE_CONSTS != 0) {
+        if (__builtin_constant_p(v.x) && v.x != 0.0f && v.x != 1.0f && v.x != -1.0f) {
+            float c = v.x;
+            asm volatile("" : "+s"(c));
+            return f2{c, c};
+        }
+    }
+    return v;
+}
 
 template <typename T>
 RB_HD Link<T> load_link(const T *__restrict__ mdl, int i) {

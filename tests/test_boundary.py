@@ -251,6 +251,10 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "rnea_lane<" in mb.jit_source(False, "rnea")         # fp32 RNEA one per lane
     assert "rnea_lane_seq2<" in mb.jit_source(True, "rnea")     # fp64 RNEA: sequential pair
     assert "rnea_lane<" in c30.jit_source(True, "rnea")         # ... up to 8 links
+    assert "rollout_lane2" in mb.jit_source(False, "rollout")   # paired fp32 rollout
+    assert "rollout_lane2" not in mb.jit_source(True, "rollout")
+    assert "rollout_lane2" not in c30.jit_source(False, "rollout")
+    assert mb.jit_compile(f64=False, kind="rollout") > 1000
     assert "sctab_init" in mb.jit_source(True, "rnea") and "sctab_init" not in mb.jit_source(False, "rnea")
     assert "RB_SPLIT_ROT 1" in mb.jit_source(False, "fd")  # FR3 frames are signed permutations
     try:
