@@ -417,10 +417,11 @@ def side_workloads(mb7, a):
     one("fd_float14_tree_f32", mbt, "fd", "f32")
     # fused rollout: K forward-dynamics + Euler steps per launch
     K, nl = 16, 40
-    w, km = time_launches(rollout_launcher(mb7, a.batch, torch.float32, K), nl, 3, 1, 300.0)
-    sec["rollout_fr3_f32_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
-                                  "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", False),
-                                  "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)"}
+    for dn, dt in (("f32", torch.float32), ("f64", torch.float64)):
+        w, km = time_launches(rollout_launcher(mb7, a.batch, dt, K), nl, 3, 1, 300.0)
+        sec[f"rollout_fr3_{dn}_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
+                                        "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", dn == "f64"),
+                                        "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)"}
     return sec
 
 

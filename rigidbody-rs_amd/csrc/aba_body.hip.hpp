@@ -218,6 +218,9 @@ __device__ __forceinline__ void aba_lane_seq2(const T *mdl, const T *__restrict_
 // ~110 VGPRs in fp32, and holding q, qd in registers across the K loop on top of them
 // costs a wave per SIMD.  Larger chains keep the state in registers.
 constexpr int kRolloutBlock = 256;
+#ifndef RB_ROLLOUT_NO_HOIST
+#define RB_ROLLOUT_NO_HOIST 0
+#endif
 
 template <typename T, int N>
 constexpr bool rollout_lds_state() {
@@ -242,12 +245,14 @@ __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T 
             sx[(N + j) * kRolloutBlock] = ld_row(qd, j * ld, off);
         }
         for (int k = 0; k < K; ++k) {
+            int64_t ldk = ld;  // RB_ROLLOUT_NO_HOIST (jit.cpp): row offsets re-derived per step
+            if constexpr (RB_ROLLOUT_NO_HOIST != 0) asm volatile("" : "+s"(ldk));
             T qv[N], qdv[N], tv[N];
 #pragma unroll
             for (int j = 0; j < N; ++j) {
                 qv[j] = sx[j * kRolloutBlock];
                 qdv[j] = sx[(N + j) * kRolloutBlock];
-                tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
+                tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ldk, off);
             }
             // aba_eval fences memory before its last pass, so these re-read LDS.
             aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T a) {
@@ -255,7 +260,7 @@ __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T 
                 const T qn = fmadd(dt, qdn, sx[j * kRolloutBlock]);
                 sx[(N + j) * kRolloutBlock] = qdn;
                 sx[j * kRolloutBlock] = qn;
-                if (traj) st_row(traj, ((int64_t)k * N + j) * ld, off, qn);
+                if (traj) st_row(traj, ((int64_t)k * N + j) * ldk, off, qn);
             });
         }
 #pragma unroll

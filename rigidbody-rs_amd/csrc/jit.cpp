@@ -47,11 +47,17 @@ int jit_nt(JitKind kind) {
     return 0;
 }
 
+// Rollouts whose K loop must not hoist anything (machine LICM off, the row stride re-derived
+// per step): the paired fp32 form, and fp64 chains up to 8 links -- 212 instead of 264 VGPRs,
+// 2 waves/SIMD instead of 1: FR3 2^20 x 16 steps 641 vs 1027 us (12 links: no change; 30
+// links, state in registers: 6.09 vs 5.81 ms, so not there).
+bool jit_rollout_no_hoist(bool f64, int n, int pack) { return pack == 2 || (f64 && n <= 8); }
+
 bool jit_opaque(JitKind kind, bool f64, int n) {
     const int v = tuning().opaque_consts;
     if (v >= 0) return v != 0;
-    (void)f64;
-    return n <= 16 && kind == JitKind::Rollout;
+    // fp64 short-chain rollouts: with hoisting off, SGPR-pinned fp64 constants only spill
+    return n <= 16 && kind == JitKind::Rollout && !(f64 && n <= 8);
 }
 
 int jit_waves(JitKind kind, bool f64, int n) {
@@ -104,6 +110,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     o << "#define RB_NT " << jit_nt(kind) << "\n";
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
     o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
+    if (kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack)) o << "#define RB_ROLLOUT_NO_HOIST 1\n";
     const bool tab = jit_f64_tab(f64);
     o << "#define RB_SINCOS_TAB " << (tab ? 1 : 0) << "\n";
     // Split joint rotation (artinertia.hip.hpp to_parent_split): pays only when every R_p is a
@@ -261,9 +268,10 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     const std::string arch_opt = "--offload-arch=" + arch;
     const char *opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffinite-math-only", "-fno-signed-zeros"};
     std::vector<const char *> optv(opts, opts + sizeof(opts) / sizeof(opts[0]));
-    // The paired rollout keeps 2 waves/SIMD only without machine LICM: hoisting per-step
-    // address arithmetic out of its K loop costs the last VGPRs below 256.
-    if (kind == JitKind::Rollout && (pack > 0 ? pack : jit_pack(kind, f64, m.n)) == 2) {
+    // The paired fp32 rollout and the fp64 rollout of short chains keep 2 waves/SIMD only
+    // without machine LICM: hoisting per-step address arithmetic and constants out of the K
+    // loop costs the VGPRs below 256 (fp64 FR3: 212 instead of 264).
+    if (kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack > 0 ? pack : jit_pack(kind, f64, m.n))) {
         optv.push_back("-mllvm");
         optv.push_back("-disable-machine-licm");
     }
