@@ -1,0 +1,21 @@
+#!/bin/bash
+# profile_round.sh for any python workload (e.g. tools/ab_bench.py --kernel rollout): a kernel
+# trace (--kernel-trace --stats) and the four separate PMC passes of the same command.
+# usage (via gpurun): tools/profile_any.sh TAG script.py [args...]
+#   outputs under gpurun_out/TAG/{trace,pmc_fetch,pmc_write,pmc_sq,pmc_grbm} + TAG_*.log
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+R=$PWD
+TAG=${1:?usage: profile_any.sh TAG script.py [args]}
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+S=$1
+shift
+B="python3 $R/$S $*"
+export TMPDIR=/tmp
+tools/gpu_steps.sh \
+  "${TAG}_trace" 300 "cd /tmp && rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B" \
+  "${TAG}_pmc_fetch" 300 "cd /tmp && rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $B" \
+  "${TAG}_pmc_write" 300 "cd /tmp && rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $B" \
+  "${TAG}_pmc_sq" 300 "cd /tmp && rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $O/pmc_sq -o run --output-format csv -- $B" \
+  "${TAG}_pmc_grbm" 300 "cd /tmp && rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS -d $O/pmc_grbm -o run --output-format csv -- $B"
