@@ -11,7 +11,7 @@ V=int(sys.argv[1]) if len(sys.argv)>1 else 128
 K=sys.argv[2] if len(sys.argv)>2 else "fd"
 soa_fn=getattr(mb, K+"_batch"); til_fn=getattr(mb, K+"_batch_tiled")
 ok=True
-for B in (1<<20, 65536, 1000, 777, 70001, 513, 256):
+for B in (1<<20, (1<<18)+777, 300001, 65536, 1000, 777, 70001, 513, 256):
     g=torch.Generator(device="cuda").manual_seed(B)
     q=torch.rand((7,B),device="cuda",generator=g)*6-3; qd=torch.rand((7,B),device="cuda",generator=g)*4-2; tau=torch.rand((7,B),device="cuda",generator=g)*20-10
     ffi.set_tuning("jit_variant",0)
