@@ -181,145 +181,6 @@ __device__ __forceinline__ void aba_lane2(const f2 *mdl, const float *__restrict
     aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
 }
 
-// Resident-grid paired forward dynamics with LDS-DMA staging (tuning jit_variant bit 8,
-// A/B).  Each wave walks pair units k = blockIdx.x, + gridDim.x, ... (unit k = batch blocks
-// 2k and 2k+1, lane t of each, as aba_lane2); the 6N input rows of unit k+1 are copied
-// global -> LDS by global_load_lds_dword (no VGPR destination) into the wave's own slot while
-// unit k computes.  Per unit the wave: waits for its staged rows, reads them into VGPRs,
-// issues the next unit's copies into the same slot, computes, stores 2N rows.  The wait is a
-// COUNTED vmcnt: the counter is shared by loads and stores and retires in issue order, so
-// waiting for the rows staged one unit ago leaves exactly the 2N stores issued after them in
-// flight (vmcnt(2N)); a vmcnt(0) there would make every unit wait for the previous unit's
-// store acknowledgements.
-template <int N>
-struct StageSlot {
-    // array a (q, qd, tau), row j, half h: floats [(16 a + 2 j + h) * 64 + lane] (N <= 8)
-    float x[3 * 16 * 64];
-};
-
-// One global_load_lds_dword per (array, row, half): 6N copies of 256 B (a lane past B points at
-// the unit's first configuration, offA = offB = 0).
-template <int N>
-__device__ __forceinline__ void stage_rows2(const float *__restrict__ q, const float *__restrict__ qd,
-                                            const float *__restrict__ tau, int64_t ld, uint32_t offA,
-                                            uint32_t offB, float *slot) {
-    using lptr = __attribute__((address_space(3))) void *;
-    const float *src[3] = {q, qd, tau};
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            gptr<const char> row = (gptr<const char>)(src[a] + j * ld);
-            __builtin_amdgcn_global_load_lds((gptr<void>)(row + offA), (lptr)(slot + (16 * a + 2 * j) * 64), 4, 0,
-                                             (RB_NT & 1) ? 2 : 0);
-            __builtin_amdgcn_global_load_lds((gptr<void>)(row + offB), (lptr)(slot + (16 * a + 2 * j + 1) * 64), 4,
-                                             0, (RB_NT & 1) ? 2 : 0);
-        }
-}
-
-// Whole units (every configuration < B), tuning jit_variant bit 11: global_load_lds_dwordx4,
-// each instruction copying four 256-B (row, half) segments of one array -- lanes 16 s .. 16 s
-// + 15 one segment -- so ceil(2N / 4) instructions per array instead of 2N.  xo[i] is the
-// lane's byte offset for instruction i from the unit's array base (loop-invariant).
-template <int N>
-__device__ __forceinline__ void stage_rows2_x4(const float *__restrict__ q, const float *__restrict__ qd,
-                                               const float *__restrict__ tau, const uint32_t (&xo)[(2 * N + 3) / 4],
-                                               float *slot) {
-    using lptr = __attribute__((address_space(3))) void *;
-    const float *src[3] = {q, qd, tau};
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int i = 0; i < (2 * N + 3) / 4; ++i)
-            __builtin_amdgcn_global_load_lds((gptr<void>)((gptr<const char>)src[a] + xo[i]),
-                                             (lptr)(slot + (16 * a + 4 * i) * 64), 16, 0, (RB_NT & 1) ? 2 : 0);
-}
-
-// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + [15:14], expcnt[6:4], lgkmcnt[11:8]).
-constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
-constexpr int kWaitLgkm0 = 15 | (3 << 14) | (7 << 4);
-
-template <int N, bool FAST, typename Topo = SerialTopo>
-__device__ __forceinline__ void aba_stage2(const f2 *mdl, const float *__restrict__ q, const float *__restrict__ qd,
-                                           const float *__restrict__ tau, float *__restrict__ qdd, uint32_t B,
-                                           int64_t ld, int64_t bs, StageSlot<N> *slots) {
-    const uint32_t units = (B + 511u) / 512u;
-    uint32_t k = blockIdx.x;
-    if (k >= units) return;
-    float *slot = slots[threadIdx.x >> 6].x;
-    const uint32_t lane = threadIdx.x & 63u;
-    // unit k's lane offsets; a lane past B evaluates the unit's first configuration and stores
-    // the bit-identical value over it (as the paired prologue in jit.cpp does for a missing half)
-    auto offs = [&](uint32_t u, uint32_t &oA, uint32_t &oB) {
-        const uint32_t bA = u * 512u + threadIdx.x;
-        oA = bA < B ? threadIdx.x * 4u : 0u;
-        oB = bA + 256u < B ? oA + (uint32_t)bs * 4u : oA;
-    };
-    uint32_t xo[(2 * N + 3) / 4];
-#pragma unroll
-    for (int i = 0; i < (2 * N + 3) / 4; ++i) {
-        const uint32_t sg = min(4u * i + (lane >> 4), 2u * N - 1u);  // segment: row sg/2, half sg%2
-        xo[i] = (uint32_t)((sg >> 1) * ld + (sg & 1u) * bs) * 4u + (threadIdx.x & ~63u) * 4u + (lane & 15u) * 16u;
-    }
-    constexpr bool kX4 = (RB_VARIANT & 2048) != 0;
-    auto stage = [&](uint32_t u, int64_t ldu, int64_t bsu, uint32_t oA, uint32_t oB) {
-        const float *qu = q + (int64_t)(2u * u) * bsu, *qdu = qd + (int64_t)(2u * u) * bsu,
-                    *tu = tau + (int64_t)(2u * u) * bsu;
-        if (kX4 && (u + 1u) * 512u <= B)
-            stage_rows2_x4<N>(qu, qdu, tu, xo, slot);
-        else
-            stage_rows2<N>(qu, qdu, tu, ldu, oA, oB, slot);
-    };
-    uint32_t offA, offB;
-    offs(k, offA, offB);
-    stage(k, ld, bs, offA, offB);
-    bool first = true;
-    for (;;) {
-        // row stride re-derived per unit (scalar ALU), so nothing row-indexed is held across units
-        int64_t ldk = ld, bsk = bs;
-        asm volatile("" : "+s"(ldk), "+s"(bsk));
-        // rows of unit k: staged before the previous unit's 2N stores (none on the first unit)
-        if (first)
-            __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-        else
-            __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * N));
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("" ::: "memory");
-        f2 qv[N], qdv[N], tv[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            qv[j] = f2{slot[(2 * j) * 64 + lane], slot[(2 * j + 1) * 64 + lane]};
-            qdv[j] = f2{slot[(16 + 2 * j) * 64 + lane], slot[(16 + 2 * j + 1) * 64 + lane]};
-            tv[j] = f2{slot[(32 + 2 * j) * 64 + lane], slot[(32 + 2 * j + 1) * 64 + lane]};
-        }
-        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // slot read out before it is overwritten
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("" ::: "memory");
-        const uint32_t kn = k + gridDim.x;
-        uint32_t offAn = 0, offBn = 0;
-        if (kn < units) {
-            offs(kn, offAn, offBn);
-            if constexpr ((RB_VARIANT & 512) == 0)  // bit 9: no staging after the first unit (A/B timing only)
-                stage(kn, ldk, bsk, offAn, offBn);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        float *out = qdd + (int64_t)(2u * k) * bsk;
-        if constexpr ((RB_VARIANT & 1024) != 0) {  // bit 10: no dynamics (A/B timing of the staging only)
-#pragma unroll
-            for (int j = 0; j < N; ++j) st_row2(out, j * ldk, offA, offB, qv[j] + qdv[j] + tv[j]);
-        } else {
-            aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 v) {
-                st_row2(out, j * ldk, offA, offB, v);
-            });
-        }
-        if (kn >= units) break;
-        k = kn;
-        offA = offAn;
-        offB = offBn;
-        first = false;
-    }
-}
-
 // Sequential pair (tuning pack=3, A/B): the configurations at byte offsets offA and offB
 // (the second only when `two`) evaluated one after the other from one load burst, so the
 // second's rows land while the first computes.

@@ -229,8 +229,7 @@ constexpr uint32_t kPackMinBatch = 1u << 18;
 
 unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
     const unsigned per_block = 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
-    const unsigned full = (unsigned)(((uint64_t)B + per_block - 1) / per_block);
-    return (jk->resident && jk->resident_blocks < full) ? jk->resident_blocks : full;
+    return (unsigned)(((uint64_t)B + per_block - 1) / per_block);
 }
 
 hipError_t jit_launch(const rbamd::JitKernel *jk, uint32_t B, void **args, hipStream_t s) {

@@ -90,12 +90,6 @@ int jit_pack(JitKind kind, bool f64, int n) {
 
 bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
 
-// Resident-grid paired FD with LDS-DMA staging (aba_body.hip.hpp aba_stage2): jit_variant
-// bit 8 (A/B).
-bool jit_staged(JitKind kind, bool f64, int n) {
-    return kind == JitKind::Fd && !f64 && n <= 8 && (tuning().jit_variant & 256) != 0;
-}
-
 std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n)) +
@@ -216,9 +210,6 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
             o << seq_prologue;
             o << "  rbamd::dev::aba_lane_seq2<T, N, " << F
               << ", Topo>(kModel, q + oA, qd + oA, tau + oA, qdd + oA, offA, offB, twoB, ld);\n}\n";
-        } else if (pack == 2 && jit_staged(kind, f64, m.n)) {
-            o << "  __shared__ rbamd::dev::StageSlot<N> slots[4];\n";
-            o << "  rbamd::dev::aba_stage2<N, " << F << ", Topo>(kModel, q, qd, tau, qdd, B, ld, bs, slots);\n}\n";
         } else if (pack == 2) {
             o << pair_prologue;
             o << "  rbamd::dev::aba_lane2<N, " << F
@@ -280,8 +271,7 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     // The paired fp32 rollout and the fp64 rollout of short chains keep 2 waves/SIMD only
     // without machine LICM: hoisting per-step address arithmetic and constants out of the K
     // loop costs the VGPRs below 256 (fp64 FR3: 212 instead of 264).
-    if ((kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack > 0 ? pack : jit_pack(kind, f64, m.n))) ||
-        ((pack > 0 ? pack : jit_pack(kind, f64, m.n)) == 2 && jit_staged(kind, f64, m.n))) {
+    if (kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack > 0 ? pack : jit_pack(kind, f64, m.n))) {
         optv.push_back("-mllvm");
         optv.push_back("-disable-machine-licm");
     }
@@ -342,15 +332,6 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack)
         jk.module = nullptr;
         jk.function = nullptr;
         return jk;
-    }
-    if (jk.pack == 2 && jit_staged(kind, f64, m.n)) {
-        int per_cu = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jk.function, 256, 0) != hipSuccess ||
-            per_cu < 1)
-            per_cu = 1;
-        const int factor = tuning().grid_factor > 0 ? tuning().grid_factor : 1;
-        jk.resident = true;
-        jk.resident_blocks = (unsigned)(per_cu * prop.multiProcessorCount * factor);
     }
     return jk;
 }

@@ -31,8 +31,6 @@ struct JitKernel {
     hipModule_t module = nullptr;
     hipFunction_t function = nullptr;  // the lane kernel (any layout)
     int pack = 1;                      // configurations per lane (2: paired fp32 lanes, 512 per block)
-    bool resident = false;             // resident grid walking units (jit_staged): grid = resident blocks
-    unsigned resident_blocks = 0;      // blocks per resident round on this device (x grid_factor)
     std::string error;                 // non-empty when compilation failed
 };
 
@@ -50,8 +48,6 @@ int jit_waves(JitKind kind, bool f64, int n);
 // Configurations per lane of `kind`'s lane kernel (tuning `pack`): 2 = paired fp32 lanes.
 int jit_pack(JitKind kind, bool f64, int n);
 std::string jit_tag(JitKind kind, bool f64, int n);
-// Resident-grid staged FD form (A/B, tuning jit_variant bit 8).
-bool jit_staged(JitKind kind, bool f64, int n);
 
 // hipRTC compilation only (no device needed): fills `code` with the code object.
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
