@@ -90,7 +90,7 @@ struct Multibody {
         std::atomic<unsigned> gen{0};
         std::atomic<const rbamd::JitKernel *> jk{nullptr};
     };
-    mutable JitSlot jit_fast[16][6][2][2][4];
+    mutable JitSlot jit_fast[16][6][2][2][4][2];  // last index: sequential-pair RNEA tail on
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
@@ -169,7 +169,9 @@ int device_consts(const Multibody *mb, const T **out) {
 // The hipRTC kernel of `kind` for this model on the current device, or nullptr (the
 // precompiled generic kernel then runs).
 // pack: configurations per lane, 0 = the jit_pack policy (jit.cpp).
-const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f64, bool fast, int pack = 0) {
+// tail: percent of a sequential-pair RNEA launch run one per lane (jit_seq_tail); other kinds 0.
+const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f64, bool fast, int pack = 0,
+                                int tail = 0) {
     if (!rbamd::jit_enabled()) return nullptr;
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
@@ -177,17 +179,18 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     const unsigned gen = rbamd::tuning_generation();
     Multibody::JitSlot *slot = nullptr;
     if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 4) {
-        slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack];
+        slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][tail > 0 ? 1 : 0];
         if (slot->gen.load(std::memory_order_acquire) == gen) return slot->jk.load(std::memory_order_relaxed);
     }
     if (pack <= 0) pack = rbamd::jit_pack(kind, f64, mb->model.n);
+    if (!(kind == rbamd::JitKind::Rnea && pack == 3)) tail = 0;
     const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
                             (fst ? ":fast" : ":precise") + rbamd::jit_tag(kind, f64, mb->model.n) + ":q" +
-                            std::to_string(pack);
+                            std::to_string(pack) + ":st" + std::to_string(tail);
     std::lock_guard<std::mutex> lk(mb->mu);
     auto it = mb->jit.find(key);
     if (it == mb->jit.end()) {
-        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, pack)).first;
+        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, pack, tail)).first;
         mb->jit_device[key] = d;
     }
     const rbamd::JitKernel *res = it->second.function ? &it->second : nullptr;
@@ -203,9 +206,9 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
 // 1024 SIMDs x 64 lanes x 2) the one-per-lane kernel keeps more of the chip busy.
 constexpr uint32_t kSeqMinBatch = 1u << 19;
 
-const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast, uint32_t B) {
+const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast, uint32_t B, bool tiled) {
     const int pack = (rbamd::tuning().pack < 0 && B < kSeqMinBatch) ? 1 : 0;
-    return jit_get(mb, rbamd::JitKind::Rnea, f64, fast, pack);
+    return jit_get(mb, rbamd::JitKind::Rnea, f64, fast, pack, rbamd::jit_seq_tail(tiled));
 }
 
 // A tree / prismatic model has no precompiled kernel: without its hipRTC kernel the launch
@@ -228,6 +231,12 @@ hipError_t no_generic(const Multibody *mb) {
 constexpr uint32_t kPackMinBatch = 1u << 18;
 
 unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
+    if (jk->pack == 3 && jk->seq_tail > 0) {  // pairs, then a one-per-lane tail (jit.cpp)
+        const unsigned T = (unsigned)(((uint64_t)B + 255u) / 256u);
+        const unsigned S = (unsigned)(((uint64_t)T * (unsigned)jk->seq_tail) / 100u);
+        const unsigned P = (T - S) & ~1u;
+        return P / 2u + (T - P);
+    }
     const unsigned per_block = 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
     return (unsigned)(((uint64_t)B + per_block - 1) / per_block);
 }
@@ -243,7 +252,7 @@ template <typename T>
 hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *qdd, T *tau,
                            uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig(), B)) {
+    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig(), B, tiled)) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&lda, (void *)&bs};
         return jit_launch(jk, B, args, s);

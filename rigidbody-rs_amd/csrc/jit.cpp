@@ -90,6 +90,12 @@ int jit_pack(JitKind kind, bool f64, int n) {
 
 bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
 
+int jit_seq_tail(bool tiled) {
+    const int v = tuning().seq_tail;
+    if (v < 0) return tiled ? 75 : 0;
+    return v < 100 ? v : 100;
+}
+
 std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n)) +
@@ -97,7 +103,7 @@ std::string jit_tag(JitKind kind, bool f64, int n) {
            std::to_string(tuning().jit_variant);
 }
 
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req) {
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req, int tail) {
     std::vector<double> pk = m.pack_f64();
     for (int i = 0; i < m.n; ++i) {
         double *c = &pk[(size_t)i * kLinkStride];
@@ -190,7 +196,23 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     const char *head = head_s.c_str();
     // Lane kernels take the block stride bs (elements): 256 for SoA, N * 256 for the tiled
     // layout (kernels.hpp); block k's arrays start at element k * bs, lane offset threadIdx.x.
-    if (kind == JitKind::Rnea && pack == 3) {
+    if (kind == JitKind::Rnea && pack == 3 && tail > 0) {
+        // pairs of tiles for blocks < G1, then one tile per block for the last S tiles
+        o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+             "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
+        o << "  const uint32_t T_ = (B + 255u) / 256u, S_ = (uint32_t)(((uint64_t)T_ * " << tail
+          << "u) / 100u);\n";
+        o << "  const uint32_t P_ = (T_ - S_) & ~1u, G1 = P_ / 2u;\n";
+        o << "  if (blockIdx.x >= G1) {\n";
+        o << "    const uint32_t t = P_ + (blockIdx.x - G1), b = t * 256u + threadIdx.x;\n";
+        o << "    if (b >= B) return;\n";
+        o << "    const int64_t o = (int64_t)t * bs;\n";
+        o << "    rbamd::dev::rnea_lane<T, N, " << F
+          << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n    return;\n  }\n";
+        o << seq_prologue;
+        o << "  rbamd::dev::rnea_lane_seq2<T, N, " << F
+          << ", Topo>(kModel, q + oA, qd + oA, qdd + oA, tau + oA, offA, offB, twoB, ld);\n}\n";
+    } else if (kind == JitKind::Rnea && pack == 3) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
         o << seq_prologue;
@@ -257,8 +279,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
 }
 
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
-                 std::vector<char> *code, std::string *error, int pack) {
-    const std::string src = jit_source(m, kind, f64, fast, pack);
+                 std::vector<char> *code, std::string *error, int pack, int tail) {
+    const std::string src = jit_source(m, kind, f64, fast, pack, tail);
     hiprtcProgram prog = nullptr;
     if (hiprtcCreateProgram(&prog, src.c_str(), "rb_jit.hip", kJitHeaderCount, kJitHeaderSources,
                             kJitHeaderNames) != HIPRTC_SUCCESS) {
@@ -308,9 +330,10 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     return true;
 }
 
-JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack) {
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack, int tail) {
     JitKernel jk;
     jk.pack = pack > 0 ? pack : jit_pack(kind, f64, m.n);
+    if (kind == JitKind::Rnea && jk.pack == 3) jk.seq_tail = tail > 0 ? tail : 0;
     int dev = 0;
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
@@ -318,7 +341,7 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack)
         return jk;
     }
     std::vector<char> code;
-    if (!jit_compile(m, kind, f64, fast, prop.gcnArchName, &code, &jk.error, jk.pack)) return jk;
+    if (!jit_compile(m, kind, f64, fast, prop.gcnArchName, &code, &jk.error, jk.pack, jk.seq_tail)) return jk;
     hipError_t e = hipModuleLoadData(&jk.module, code.data());
     if (e != hipSuccess) {
         jk.error = std::string("hipModuleLoadData: ") + hipGetErrorString(e);

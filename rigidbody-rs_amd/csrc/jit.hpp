@@ -31,6 +31,7 @@ struct JitKernel {
     hipModule_t module = nullptr;
     hipFunction_t function = nullptr;  // the lane kernel (any layout)
     int pack = 1;                      // configurations per lane (2: paired fp32 lanes, 512 per block)
+    int seq_tail = 0;                  // pack 3: trailing tiles run one per lane (tuning seq_tail)
     std::string error;                 // non-empty when compilation failed
 };
 
@@ -38,7 +39,8 @@ bool jit_enabled();
 
 // Generated HIP source for one specialised kernel (exposed for tests / inspection).
 // pack: configurations per lane, 0 = the jit_pack policy.
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0);
+// tail: sequential-pair RNEA only -- percent of the launch's tiles run one per lane (0 none).
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0);
 
 // Non-temporal access bits of `kind`'s JIT source, and the cache-key suffix of every
 // tuning value that changes the source (tuning.hpp).
@@ -48,12 +50,15 @@ int jit_waves(JitKind kind, bool f64, int n);
 // Configurations per lane of `kind`'s lane kernel (tuning `pack`): 2 = paired fp32 lanes.
 int jit_pack(JitKind kind, bool f64, int n);
 std::string jit_tag(JitKind kind, bool f64, int n);
+// Percent of a sequential-pair RNEA launch's tiles run one per lane for this layout (tuning
+// seq_tail; auto: 75 for the tiled layout, 0 for SoA).
+int jit_seq_tail(bool tiled);
 
 // hipRTC compilation only (no device needed): fills `code` with the code object.
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
-                 std::vector<char> *code, std::string *error, int pack = 0);
+                 std::vector<char> *code, std::string *error, int pack = 0, int tail = 0);
 
 // Compiles and loads the kernel on the current device.  Never throws.
-JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0);
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0);
 
 }  // namespace rbamd

@@ -44,6 +44,7 @@ const Key kKeys[] = {
     {"f64_tab", &Tuning::f64_tab, true},
     {"split_rot", &Tuning::split_rot, true},
     {"jit_variant", &Tuning::jit_variant, true},
+    {"seq_tail", &Tuning::seq_tail, true},
 };
 
 // RB_<KEY> environment overrides (upper-cased key), experimental ones only with RB_EXPERIMENTAL=1.

@@ -51,6 +51,12 @@ struct Tuning {
     int split_rot = -1;
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
     int jit_variant = 0;
+    // Sequential-pair RNEA (pack 3): the last `seq_tail` percent of a launch's 256-configuration
+    // tiles run one configuration per lane, so the blocks dispatched last carry half the
+    // dependent chain (the launch's compute tail after its last rows land).  0 = all pairs,
+    // -1 auto: 75 for the tiled layout (FR3 fp64 2^20: 40.5 vs 41.8 us), 0 for SoA (43.6-45.9 vs
+    // 42.9 us), DESIGN.md §4.
+    int seq_tail = -1;
 };
 
 // Process-wide knobs, initialised from RB_JIT / RB_PACK / RB_RNEA_STREAM (and, with
