@@ -602,6 +602,33 @@ def test_single_config_host_vs_gpu(ffi, dev, fr3_text):
         assert np.abs(host[b][1] - H[:, b]).max() <= 1e-14 * (1 + np.abs(H[:, b]).max()), b
 
 
+def test_single_tail_grid_bit_identical(ffi, dev, fr3_text):
+    """The fp64 RNEA auto policy at batches >= 2^19 on the tiled layout: sequential pairs for the
+    first quarter of the tiles, one configuration per lane for the rest (tuning seq_tail, the
+    headline's grid).  Bit-identical to the SoA launch (all-pair grid) and to the one-per-lane
+    grid (pack=1) at the bench size and on ragged batches where the pair/single boundary and
+    the last tile are partial; oracle spot columns at both ends."""
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    om = _oracle(fr3_text)
+    try:
+        for B in ((1 << 20), (1 << 19) + 333, (1 << 19) + 256 * 3 + 17):
+            g = torch.Generator(device=dev).manual_seed(B)
+            x = [(torch.rand((7, B), device=dev, generator=g, dtype=torch.float64) * 4 - 2) for _ in range(3)]
+            xt = [ffi.to_tiled(a) for a in x]
+            tail = ffi.from_tiled(mb.rnea_batch_tiled(*xt, B), B)
+            pairs = mb.rnea_batch(*x)
+            ffi.set_tuning("pack", 1)
+            single = ffi.from_tiled(mb.rnea_batch_tiled(*xt, B), B)
+            ffi.set_tuning("pack", -1)
+            assert torch.equal(tail, pairs), B
+            assert torch.equal(tail, single), B
+            cols = np.r_[np.arange(300), np.arange(B - 300, B)]
+            xs = [a[:, cols].cpu().numpy() for a in x]
+            _close(tail[:, cols].cpu().numpy(), om.rnea_batch(*xs), 1e-9, f"single-tail grid B={B}")
+    finally:
+        ffi.set_tuning("pack", -1)
+
+
 @pytest.mark.parametrize("kind", ["rnea", "fd"])
 def test_sequential_pair_bit_identical(kind, ffi, dev, fr3_text):
     """Two configurations per lane evaluated one after the other (tuning pack=3: lane t of
