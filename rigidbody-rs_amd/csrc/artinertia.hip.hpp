@@ -146,6 +146,64 @@ RB_HD ArtI<T> to_parent_split(const M3<T> &Rp, T c, T s, const M3<T> &E, const V
     return o;
 }
 
+// ------------------------------------------------- composite rigid body (CRBA) helpers
+// A composite of rigid bodies is rigid: mass m, first moment h = m c and the inertia I_o
+// about the link origin (Inertia {mass, com, inertia}, inertia.rs:12-18) -- 10 values where
+// the articulated block form carries 21, and m is a compile-time constant in the
+// model-specialised kernels (a sum of link masses).
+template <typename T>
+struct RigidI {
+    T m;
+    V3<T> h;
+    S3<T> Io;
+};
+
+template <typename T>
+RB_HD RigidI<T> rigid_of(const Link<T> &L) {
+    return RigidI<T>{L.m, L.h, L.Io};
+}
+
+// X^T I X for the child->parent transform (E, p) (Inertia::transform, inertia.rs:81-89):
+// rotate, h1 = E h, Io1 = E Io E^T, then move the reference point by p (parallel axis):
+//   h'  = h1 + m p
+//   Io' = Io1 - (h1 p^T + p h1^T) - m p p^T + (2 p.h1 + m |p|^2) 1
+// With RB_SPLIT_ROT the rotation is R_p (Rz S Rz^T) R_p^T (rot_sym_z), as to_parent_split.
+template <typename T>
+RB_HD RigidI<T> rigid_to_parent(const M3<T> &Rp, T c, T s, const M3<T> &E, const V3<T> &p, const RigidI<T> &I) {
+    S3<T> Io1;
+    V3<T> h1;
+    if constexpr (RB_SPLIT_ROT != 0) {
+        const T C = fmadd(c, c, -s * s), S2 = (c + c) * s;
+        Io1 = rot_sym(Rp, rot_sym_z(c, s, C, S2, I.Io));
+        h1 = mul(Rp, v3(fmadd(c, I.h.x, -s * I.h.y), fmadd(s, I.h.x, c * I.h.y), I.h.z));
+    } else {
+        Io1 = rot_sym(E, I.Io);
+        h1 = mul(E, I.h);
+    }
+    const T m = I.m;
+    const T d = fmadd(T(2) * p.x, h1.x, fmadd(T(2) * p.y, h1.y, fmadd(T(2) * p.z, h1.z,
+                      m * fmadd(p.x, p.x, fmadd(p.y, p.y, p.z * p.z)))));
+    const T mpx = m * p.x, mpy = m * p.y, mpz = m * p.z;
+    RigidI<T> o;
+    o.m = m;
+    o.h = v3(h1.x + mpx, h1.y + mpy, h1.z + mpz);
+    o.Io = S3<T>{fmadd(-(h1.x + h1.x + mpx), p.x, Io1.xx + d),
+                 fmadd(-(h1.x + mpx), p.y, fmadd(-h1.y, p.x, Io1.xy)),
+                 fmadd(-(h1.x + mpx), p.z, fmadd(-h1.z, p.x, Io1.xz)),
+                 fmadd(-(h1.y + h1.y + mpy), p.y, Io1.yy + d),
+                 fmadd(-(h1.y + mpy), p.z, fmadd(-h1.z, p.y, Io1.yz)),
+                 fmadd(-(h1.z + h1.z + mpz), p.z, Io1.zz + d)};
+    return o;
+}
+
+template <typename T>
+RB_HD void add_rigid(RigidI<T> &I, const Link<T> &L) {
+    I.m += L.m;
+    I.h = v3(I.h.x + L.h.x, I.h.y + L.h.y, I.h.z + L.h.z);
+    I.Io.xx += L.Io.xx; I.Io.xy += L.Io.xy; I.Io.xz += L.Io.xz;
+    I.Io.yy += L.Io.yy; I.Io.yz += L.Io.yz; I.Io.zz += L.Io.zz;
+}
+
 template <typename T>
 RB_HD void add_rigid(ArtI<T> &I, const Link<T> &L) {
     I.A.xx += L.Io.xx; I.A.xy += L.Io.xy; I.A.xz += L.Io.xz;

@@ -9,21 +9,20 @@
 namespace rbamd {
 namespace dev {
 
-template <typename T, int N, bool FAST, typename Out>
-RB_HD void crba_eval(const T *mdl, const T (&qv)[N], Out &&out) {
-    T cs[N], sn[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);
-
-    ArtI<T> Ic = rigid_inertia(load_link(mdl, N - 1));
+// The recursion on given joint (cos, sin): also the mass-matrix stage of the forward dynamics
+// (fdh_body.hip.hpp), which has them from its bias-torque sweep.
+template <typename T, int N, typename Out>
+RB_HD void crba_core(const T *mdl, const T (&cs)[N], const T (&sn)[N], Out &&out) {
+    RigidI<T> Ic = rigid_of(load_link(mdl, N - 1));  // composite rigid body (artinertia.hip.hpp)
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
         reload_fence();
-        out(i + N * i, Ic.A.zz);  // get_rotz, inertia.rs:91-93
+        out(i + N * i, Ic.Io.zz);  // get_rotz, inertia.rs:91-93
 #pragma unroll
         for (int r = i + 1; r < N; ++r) out(r + N * i, T(0));
-        V3<T> Fn = v3(Ic.A.xz, Ic.A.yz, Ic.A.zz);
-        V3<T> Ff = v3(Ic.B.m[6], Ic.B.m[7], Ic.B.m[8]);
+        // F = Ic S, S = rot z:  n = I_o e_z,  f = -h x e_z = (-h.y, h.x, 0)
+        V3<T> Fn = v3(Ic.Io.xz, Ic.Io.yz, Ic.Io.zz);
+        V3<T> Ff = v3(-Ic.h.y, Ic.h.x, T(0));
 #pragma unroll
         for (int j = i - 1; j >= 0; --j) {
             const Link<T> L = load_link(mdl, j + 1);
@@ -36,13 +35,18 @@ RB_HD void crba_eval(const T *mdl, const T (&qv)[N], Out &&out) {
         if (i > 0) {
             const Link<T> L = load_link(mdl, i);
             const M3<T> E = joint_rotation(L.Rp, cs[i], sn[i]);
-            if constexpr (RB_SPLIT_ROT != 0)
-                Ic = to_parent_split(L.Rp, cs[i], sn[i], E, L.p, Ic);
-            else
-                Ic = to_parent(E, L.p, Ic);
+            Ic = rigid_to_parent(L.Rp, cs[i], sn[i], E, L.p, Ic);
             add_rigid(Ic, load_link(mdl, i - 1));
         }
     }
+}
+
+template <typename T, int N, bool FAST, typename Out>
+RB_HD void crba_eval(const T *mdl, const T (&qv)[N], Out &&out) {
+    T cs[N], sn[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);
+    crba_core<T, N>(mdl, cs, sn, static_cast<Out &&>(out));
 }
 
 template <typename T, int N, bool FAST, typename Topo = SerialTopo>

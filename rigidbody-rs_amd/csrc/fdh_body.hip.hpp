@@ -1,0 +1,176 @@
+// fdh_body.hip.hpp -- per-lane forward dynamics by the mass-matrix method (device).
+//
+// The reference has no forward-dynamics solve; SURVEY §8(a) A10 defines it as
+//     qdd = sym(H)^-1 (tau - rnea(q, qd, 0))
+// with H from Multibody::crba (multibody.rs:155-174) and the bias torques from
+// Multibody::rnea (multibody.rs:111-153) at zero joint acceleration.  This lane body
+// evaluates exactly that definition, fused in registers:
+//   1. bias torques C = rnea(q, qd, 0): the RNEA sweeps of rnea_body.hip.hpp with qdd = 0
+//      (the fictitious-gravity base acceleration, multibody.rs:117-120, stays);
+//   2. H by composite rigid bodies (crba_body.hip.hpp crba_core) on the same (cos, sin);
+//   3. H = L D L^T (unit lower L, no square roots) and two triangular solves on tau - C.
+// Against the Articulated-Body form (aba_body.hip.hpp) it carries far less per-lane state
+// across its sweeps -- no per-link articulated inertias or pass-3 projections, the peak is
+// the n(n+1)/2 entries of H -- so short chains run at 2-3x the ABA's waves per SIMD; its
+// mass-matrix stage grows as n^2, so long chains keep the ABA (jit.cpp jit_fd_form).
+//
+// Order of work follows the order the rows land: q, qd root->leaf first (the bias sweep's
+// first-use order), tau only after that sweep -- it enters at the final solve.
+#pragma once
+
+#include "crba_body.hip.hpp"
+#include "rnea_body.hip.hpp"
+
+namespace rbamd {
+namespace dev {
+
+// Where the tau rows are loaded: 1 = after the bias sweep (default), 0 = with q and qd at the
+// start, 2 = after the mass matrix (jit_variant bits 0-1 = 1 / 2 select 0 / 2, A/B only).
+// After the bias sweep the rows are not held across it (fp64: 121 instead of 134 VGPRs, 4
+// waves/SIMD instead of 3) and still land under the mass-matrix stage: FR3 2^20 tiled, fp64
+// 56.2 vs 57.0 us, fp32 paired 27.1 vs 28.1 us; at 65536 (fp32) 4.52 vs 4.63 us, while loading
+// after the mass matrix exposes the latency there (4.90 us).
+#ifndef RB_FDH_TAU_AT
+#define RB_FDH_TAU_AT ((RB_VARIANT & 3) == 1 ? 0 : (RB_VARIANT & 3) == 2 ? 2 : 1)
+#endif
+
+template <typename T, int N, bool FAST, typename Tau, typename Out>
+RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&load_tau, Out &&out) {
+    T cs[N], sn[N], C[N], tv[N];
+    if constexpr (RB_FDH_TAU_AT == 0) load_tau(tv);
+    // 1. bias torques (multibody.rs:111-153 with ddq = 0)
+    {
+        V3<T> fn[N], ff[N];
+        RneaState<T> st;
+        rnea_fwd0<T, FAST>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0]);
+#pragma unroll
+        for (int j = 1; j < N; ++j) rnea_fwd<T, FAST>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j]);
+        reload_fence();
+#pragma unroll
+        for (int j = N - 1; j >= 1; --j) {
+            C[j] = fn[j].z;
+            rnea_bwd(mdl, j, cs[j], sn[j], ff[j], fn[j], ff[j - 1], fn[j - 1]);
+        }
+        C[0] = fn[0].z;
+    }
+    if constexpr (RB_FDH_TAU_AT == 1) load_tau(tv);
+    // 2. joint-space inertia, upper triangle H[j][i] (j <= i) of the ABI's column-major matrix
+    T H[N][N];
+    reload_fence();
+    crba_core<T, N>(mdl, cs, sn, [&](int e, T v) {
+        const int j = e % N, i = e / N;
+        if (j <= i) H[j][i] = v;
+    });
+    if constexpr (RB_FDH_TAU_AT >= 2) load_tau(tv);
+    // 3. H = L D L^T, root first: L[i][j] (i > j) overwrites H[j][i]; Di = 1 / D[j]
+    T D[N], Di[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        T w[N];  // w[k] = L[j][k] D[k]
+        T d = H[j][j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) {
+            w[k] = H[k][j] * D[k];
+            d = fmadd(-H[k][j], w[k], d);
+        }
+        D[j] = d;
+        Di[j] = recip(d);
+#pragma unroll
+        for (int i = j + 1; i < N; ++i) {
+            T s = H[j][i];
+#pragma unroll
+            for (int k = 0; k < j; ++k) s = fmadd(-H[k][i], w[k], s);
+            H[j][i] = s * Di[j];
+        }
+    }
+    // 4. L y = tau - C,  z = D^-1 y,  L^T x = z  (x = qdd)
+    T x[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        T y = tv[i] - C[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) y = fmadd(-H[k][i], x[k], y);
+        x[i] = y;
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        T z = x[i] * Di[i];
+#pragma unroll
+        for (int k = i + 1; k < N; ++k) z = fmadd(-H[i][k], x[k], z);
+        x[i] = z;
+        out(i, z);
+    }
+}
+
+// Lane body: loads in first-use order (q, qd root->leaf, then tau), as aba_lane.
+// Decomposition variants (jit_variant, A/B only): bit 2 = no input loads (inputs synthesised
+// from the lane index: compute + stores), bit 3 = no dynamics (loads + stores of their sum).
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void fdh_lane(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                         const T *__restrict__ tau, T *__restrict__ qdd, uint32_t b, int64_t ld) {
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    T qv[N], qdv[N];
+    if constexpr ((RB_VARIANT & 4) != 0) {
+        const T x = T((b + blockIdx.x) & 1023u) * T(1e-3);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = x + T(0.1) * T(j) - T(0.5);
+            qdv[j] = T(0.7) - x - T(0.05) * T(j);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+            qdv[j] = ld_row(qd, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    auto load_tau = [&](T (&tv)[N]) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            if constexpr ((RB_VARIANT & 4) != 0) {
+                tv[j] = qv[N - 1 - j] * T(3);
+            } else {
+                tv[j] = ld_row(tau, j * ld, off);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    };
+    if constexpr ((RB_VARIANT & 8) != 0) {
+        T tv[N];
+        load_tau(tv);
+#pragma unroll
+        for (int j = 0; j < N; ++j) st_row(qdd, j * ld, off, qv[j] + qdv[j] + tv[j]);
+    } else {
+        fdh_eval<T, N, FAST>(mdl, qv, qdv, load_tau, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
+    }
+}
+
+// Paired lane (packed fp32, spatial.hip.hpp f2), as aba_lane2.
+template <int N, bool FAST>
+__device__ __forceinline__ void fdh_lane2(const f2 *mdl, const float *__restrict__ q, const float *__restrict__ qd,
+                                          const float *__restrict__ tau, float *__restrict__ qdd, uint32_t offA,
+                                          uint32_t offB, int64_t ld) {
+    f2 qv[N], qdv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qv[j] = ld_row2(q, j * ld, offA, offB);
+        __builtin_amdgcn_sched_barrier(0);
+        qdv[j] = ld_row2(qd, j * ld, offA, offB);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    fdh_eval<f2, N, FAST>(
+        mdl, qv, qdv,
+        [&](f2 (&tv)[N]) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                tv[j] = ld_row2(tau, j * ld, offA, offB);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        },
+        [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
+}
+
+}  // namespace dev
+}  // namespace rbamd

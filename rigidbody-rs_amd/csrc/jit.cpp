@@ -90,17 +90,36 @@ int jit_pack(JitKind kind, bool f64, int n) {
 
 bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
 
+int jit_fd_form(const Model &m) {
+    // 2 = mass-matrix forward dynamics (fdh_body.hip.hpp: RNEA bias + CRBA + L D L^T), 1 = the
+    // Articulated-Body Algorithm (aba_body.hip.hpp).  The mass-matrix form holds ~n^2/2 values
+    // per lane where the ABA holds ~12 per link across its sweeps, so it runs at 2-3x the
+    // ABA's waves per SIMD on short chains; its O(n^2) work loses on long ones.  Trees keep
+    // the ABA (tree_body.hip.hpp).
+    if (!m.serial_revolute()) return 1;
+    const int v = tuning().fd_form;
+    if (v == 1 || v == 2) return v;
+    return m.n <= 8 ? 2 : 1;
+}
+
 int jit_seq_tail(bool tiled) {
     const int v = tuning().seq_tail;
     if (v < 0) return tiled ? 75 : 0;
     return v < 100 ? v : 100;
 }
 
+int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
+    const int pack = pack_req > 0 ? pack_req : jit_pack(kind, f64, m.n);
+    // the mass-matrix forward dynamics has one- and two-per-lane forms only
+    if (kind == JitKind::Fd && pack == 3 && jit_fd_form(m) == 2) return 1;
+    return pack;
+}
+
 std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n)) +
            ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":r" + std::to_string(tuning().split_rot) + ":v" +
-           std::to_string(tuning().jit_variant);
+           std::to_string(tuning().jit_variant) + ":f" + std::to_string(tuning().fd_form);
 }
 
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req, int tail) {
@@ -111,7 +130,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         for (int k = 0; k < 3; ++k) c[kP + k] = snap(c[kP + k]);
     }
     const char *F = fast ? "true" : "false";
-    const int pack = pack_req > 0 ? pack_req : jit_pack(kind, f64, m.n);
+    const int pack = jit_model_pack(m, kind, f64, pack_req);
+    const bool fdh = kind == JitKind::Fd && jit_fd_form(m) == 2;
     std::ostringstream o;
     o << "#define RB_NT " << jit_nt(kind) << "\n";
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
@@ -136,6 +156,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     const int sr = tuning().split_rot;
     o << "#define RB_SPLIT_ROT " << ((sr > 0 || (sr < 0 && perm)) ? 1 : 0) << "\n";
     o << (kind == JitKind::Rnea                               ? "#include \"rnea_body.hip.hpp\"\n"
+          : fdh                                               ? "#include \"fdh_body.hip.hpp\"\n"
           : (kind == JitKind::Fd || kind == JitKind::Rollout) ? "#include \"aba_body.hip.hpp\"\n"
           : kind == JitKind::Crba                             ? "#include \"crba_body.hip.hpp\"\n"
                                                               : "#include \"tree_body.hip.hpp\"\n");
@@ -228,7 +249,15 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
-        if (pack == 3) {
+        if (fdh && pack == 2) {
+            o << pair_prologue;
+            o << "  rbamd::dev::fdh_lane2<N, " << F << ">(kModel, q + oA, qd + oA, tau + oA, qdd + oA, offA, offB, ld);\n}\n";
+        } else if (fdh) {
+            o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+            o << "  if (b >= B) return;\n";
+            o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+            o << "  rbamd::dev::fdh_lane<T, N, " << F << ">(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
+        } else if (pack == 3) {
             o << seq_prologue;
             o << "  rbamd::dev::aba_lane_seq2<T, N, " << F
               << ", Topo>(kModel, q + oA, qd + oA, tau + oA, qdd + oA, offA, offB, twoB, ld);\n}\n";
@@ -332,7 +361,7 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
 
 JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack, int tail) {
     JitKernel jk;
-    jk.pack = pack > 0 ? pack : jit_pack(kind, f64, m.n);
+    jk.pack = jit_model_pack(m, kind, f64, pack);
     if (kind == JitKind::Rnea && jk.pack == 3) jk.seq_tail = tail > 0 ? tail : 0;
     int dev = 0;
     hipDeviceProp_t prop;

@@ -36,6 +36,7 @@ const Key kKeys[] = {
     {"pack", &Tuning::pack, false},
     {"rnea_stream", &Tuning::rnea_stream, false},
     {"single_gpu", &Tuning::single_gpu, false},
+    {"fd_form", &Tuning::fd_form, false},
     {"grid_factor", &Tuning::grid_factor, true},
     {"rnea_nt", &Tuning::rnea_nt, true},
     {"fd_nt", &Tuning::fd_nt, true},

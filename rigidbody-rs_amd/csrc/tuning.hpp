@@ -1,7 +1,7 @@
 // tuning.hpp -- launch-shape knobs (host side) and resident-grid sizing.
 //
 // Production knobs (rb_set_tuning accepts these always): `jit`, `pack`, `rnea_stream`,
-// `single_gpu`.
+// `single_gpu`, `fd_form`.
 // Everything else is an A/B experiment selector: rb_set_tuning accepts it only when the
 // process runs with RB_EXPERIMENTAL=1 (tools/ab_bench.py, tools/small_batch.py), so a normal
 // caller cannot multiply the hipRTC kernel variants (jit.cpp cache key) or the test matrix.
@@ -25,6 +25,11 @@ struct Tuning {
     // host thread with the lane bodies compiled for the host (host_eval.cpp) where the model
     // allows it, 1 = always a GPU launch (H2D, kernel, D2H, sync).
     int single_gpu = 0;
+    // Forward dynamics algorithm of the model-specialised kernels: 1 = Articulated-Body
+    // Algorithm (aba_body.hip.hpp), 2 = mass-matrix method (fdh_body.hip.hpp: bias torques by
+    // RNEA, H by CRBA, L D L^T solve -- the oracle's own definition), -1 auto (jit.cpp
+    // jit_fd_form: mass matrix for serial chains up to 8 links).
+    int fd_form = -1;
 
     // ---- experimental (RB_EXPERIMENTAL=1)
     int grid_factor = 1;  // streaming grid = grid_factor x resident blocks (capped by the batch)

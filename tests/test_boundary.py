@@ -207,9 +207,17 @@ def test_jit_source_and_compile(ffi, fr3_text):
     for kind in ("rnea", "fd", "crba", "rollout"):
         for f64 in (False, True):
             assert mb.jit_compile(f64=f64, kind=kind) > 1000
-    assert "aba_lane" in mb.jit_source(kind="fd") and "crba_lane" in mb.jit_source(kind="crba")
+    # FR3 forward dynamics: the mass-matrix form by default, the ABA under fd_form 1
+    assert "fdh_lane" in mb.jit_source(kind="fd") and "crba_lane" in mb.jit_source(kind="crba")
+    try:
+        ffi.set_tuning("fd_form", 1)
+        assert "aba_lane" in mb.jit_source(kind="fd")
+        assert mb.jit_compile(f64=True, kind="fd") > 1000
+    finally:
+        ffi.set_tuning("fd_form", -1)
     c30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     assert "rnea_lane" in c30.jit_source(f64=False)  # JIT kernels use the one-per-lane form
+    assert "aba_lane" in c30.jit_source(kind="fd")  # long chains keep the ABA
     assert c30.jit_compile(f64=False) > 1000
 
 
@@ -245,9 +253,9 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
 
     mb = ffi.Multibody.from_urdf_string(fr3_text)
     c30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
-    assert "aba_lane2" in mb.jit_source(False, "fd")            # auto policy: paired FD
-    assert "aba_lane2" not in c30.jit_source(False, "fd")       # ... not for 30 links
-    assert "aba_lane2" not in mb.jit_source(True, "fd")         # ... nor fp64
+    assert "fdh_lane" in mb.jit_source(False, "fd")             # FR3: mass-matrix FD
+    assert "fdh_lane" in mb.jit_source(True, "fd")
+    assert "fdh_lane" not in c30.jit_source(False, "fd")        # ... the ABA for 30 links
     assert "rnea_lane<" in mb.jit_source(False, "rnea")         # fp32 RNEA one per lane
     assert "rnea_lane_seq2<" in mb.jit_source(True, "rnea")     # fp64 RNEA: sequential pair
     assert "rnea_lane<" in c30.jit_source(True, "rnea")         # ... up to 8 links
@@ -258,14 +266,17 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "sctab_init" in mb.jit_source(True, "rnea") and "sctab_init" not in mb.jit_source(False, "rnea")
     assert "RB_SPLIT_ROT 1" in mb.jit_source(False, "fd")  # FR3 frames are signed permutations
     try:
-        for pack, marker in ((2, "aba_lane2"), (1, "aba_lane<"), (3, "aba_lane_seq2<")):
+        for form, pack, marker in ((1, 2, "aba_lane2"), (1, 1, "aba_lane<"), (1, 3, "aba_lane_seq2<"),
+                                   (2, 2, "fdh_lane2<"), (2, 1, "fdh_lane<")):
+            ffi.set_tuning("fd_form", form)
             ffi.set_tuning("pack", pack)
-            assert marker in mb.jit_source(False, "fd"), pack
-            assert mb.jit_compile(f64=False, kind="fd") > 1000, pack
+            assert marker in mb.jit_source(False, "fd"), (form, pack)
+            assert mb.jit_compile(f64=False, kind="fd") > 1000, (form, pack)
         ffi.set_tuning("pack", 1)
         assert "rnea_lane<" in mb.jit_source(True, "rnea")
     finally:
         ffi.set_tuning("pack", -1)
+        ffi.set_tuning("fd_form", -1)
     for kind in ("rnea", "fd", "crba", "rollout"):
         assert mb.jit_compile(f64=True, kind=kind) > 1000, kind
 

@@ -662,3 +662,96 @@ def test_sequential_pair_bit_identical(kind, ffi, dev, fr3_text):
             else:
                 res = om.rnea_batch(xs[0], xs[1], v.cpu().numpy()) - xs[2]
                 assert (np.abs(res) / (1 + np.abs(xs[2]))).max() <= 1e-8, (B, lay)
+
+
+# ------------------------------------------------------------ forward-dynamics forms
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_fd_forms_vs_oracle(dt, ffi, dev, fr3_text):
+    """Both forward-dynamics algorithms of the model-specialised kernels (tuning fd_form):
+    1 = Articulated-Body Algorithm (aba_body.hip.hpp), 2 = the mass-matrix method
+    (fdh_body.hip.hpp: rnea(q, qd, 0) bias, CRBA H, L D L^T solve -- the oracle's own
+    definition, SURVEY §8(a) A10 over multibody.rs:111-174), fp32 with one and two
+    configurations per lane, SoA and tiled, at B = 1, 255, 65536 (config 3) and the ragged
+    65539, against the oracle's CRBA solve:
+      fp64: |qdd - qdd_oracle| <= 1e-9 max(1, cond(H)/1e3) (1 + |qdd|), torque residual 1e-8;
+      fp32: the backward-error bound K <= 16 and the element-wise 1e-3 torque residual.
+    SoA and tiled outputs of one kernel form are bit-identical."""
+    from rigidbody_amd import chains
+
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    om = _oracle(fr3_text)
+    lim = mb.limits()
+    dtype = torch.float64 if dt == "f64" else torch.float32
+    npd = "float64" if dt == "f64" else "float32"
+    packs = (1,) if dt == "f64" else (1, 2)
+    outs = {}
+    try:
+        for form in (1, 2):
+            ffi.set_tuning("fd_form", form)
+            for pack in packs:
+                ffi.set_tuning("pack", pack)
+                for B in (1, 255, 65536, 65539):
+                    x = [chains.host_uniform(7, B, *chains.input_ranges(lim, k), chains.SEED + 11 + i, dtype=npd)
+                         for i, k in enumerate(("q", "qd", "tau"))]
+                    xt = [_t(a, dev, dtype) for a in x]
+                    soa = mb.fd_batch(*xt).cpu().numpy()
+                    til = ffi.from_tiled(mb.fd_batch_tiled(*[ffi.to_tiled(a) for a in xt], B), B).cpu().numpy()
+                    assert mb.kernel_path("fd", dt == "f64") == "jit", ffi.last_error()
+                    np.testing.assert_array_equal(soa, til, err_msg=f"form={form} pack={pack} B={B}")
+                    outs[(form, pack, B)] = ([a.astype(np.float64) for a in x], soa.astype(np.float64))
+    finally:
+        ffi.set_tuning("fd_form", -1)
+        ffi.set_tuning("pack", -1)
+    for (form, pack, B), (x, qdd) in outs.items():
+        what = f"{dt} form={form} pack={pack} B={B}"
+        assert np.all(np.isfinite(qdd)), what
+        ref = om.fd_batch(*x)
+        res = om.rnea_batch(x[0], x[1], qdd) - x[2]
+        Hraw = om.crba_batch(x[0])
+        if dt == "f64":
+            Hm = Hraw.reshape(7, 7, B).transpose(2, 1, 0)
+            cond = np.linalg.cond(np.triu(Hm) + np.transpose(np.triu(Hm, 1), (0, 2, 1)))
+            err = np.abs(qdd - ref).max(0) / (1 + np.abs(ref).max(0))
+            assert (err <= 1e-9 * np.maximum(1.0, cond / 1e3)).all(), (what, err.max())
+            assert (np.abs(res) / (1 + np.abs(x[2]))).max() <= 1e-8, what
+        else:
+            assert (np.abs(res) / (1 + np.abs(x[2]))).max() <= 1e-3, what
+            assert fp32_fd_backward_ratio(res, Hraw, qdd, x[2]).max() <= FD32_BACKWARD_K, what
+
+
+def test_fd_mass_matrix_full_size_f64(ffi, dev, fr3_text):
+    """The mass-matrix forward dynamics (fd_form 2, the FR3 default) at BASELINE config 4's
+    size, B = 2^20 fp64, on every column: the fd -> rnea round trip reproduces tau to 1e-8
+    (scaled) and agrees with the Articulated-Body kernel to 1e-9 max(1, cond/1e3) on 4096 spot
+    columns checked against the oracle (multibody.rs:111-174)."""
+    from rigidbody_amd import chains
+
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    lim = mb.limits()
+    B = 1 << 20
+    x = {}
+    for k, kind in enumerate(("q", "qd", "tau")):
+        lo, hi = chains.input_ranges(lim, kind)
+        x[kind] = ffi.fill_uniform(torch.empty((7, B), dtype=torch.float64, device=dev), lo, hi, chains.SEED + 40 + k)
+    got = {}
+    try:
+        for form in (2, 1):
+            ffi.set_tuning("fd_form", form)
+            got[form] = mb.fd_batch(x["q"], x["qd"], x["tau"])
+    finally:
+        ffi.set_tuning("fd_form", -1)
+    back = mb.rnea_batch(x["q"], x["qd"], got[2])
+    rt = ((back - x["tau"]).abs() / (1 + x["tau"].abs())).max().item()
+    assert rt <= 1e-8, rt
+    idx = torch.linspace(0, B - 1, 4096, device=dev).long()
+    om = _oracle(fr3_text)
+    xs = [x[k][:, idx].cpu().numpy() for k in ("q", "qd", "tau")]
+    ref = om.fd_batch(*xs)
+    Hm = om.crba_batch(xs[0]).reshape(7, 7, -1).transpose(2, 1, 0)
+    cond = np.linalg.cond(np.triu(Hm) + np.transpose(np.triu(Hm, 1), (0, 2, 1)))
+    for form in (2, 1):
+        g = got[form][:, idx].cpu().numpy()
+        err = np.abs(g - ref).max(0) / (1 + np.abs(ref).max(0))
+        assert (err <= 1e-9 * np.maximum(1.0, cond / 1e3)).all(), (form, err.max(), cond.max())
+    d = ((got[2] - got[1]).abs() / (1 + got[1].abs())).max().item()
+    print(f"fd mass-matrix f64 2^20: round trip {rt:.2e}, vs ABA {d:.2e}")
