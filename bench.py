@@ -357,17 +357,33 @@ def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED):
     return launch
 
 
+# Timed work of every secondary line, independent of --steps (the driver runs --steps 20): at
+# least SIDE_MIN_LAUNCHES launches and at least SIDE_TARGET_MS of them.
+SIDE_TARGET_MS = 60.0
+SIDE_MIN_LAUNCHES = 200
+SIDE_MAX_LAUNCHES = 40000
+
+
+def budget_steps(launch, target_ms=SIDE_TARGET_MS, lo=SIDE_MIN_LAUNCHES, hi=SIDE_MAX_LAUNCHES):
+    """Launch count for ~target_ms of timed work, from a 20-launch calibration."""
+    _, ms = time_launches(launch, 20, 3, 1, 0.0)
+    return int(min(hi, max(lo, np.ceil(target_ms / max(ms, 1e-4)))))
+
+
 def measure(mb, kernel, dt_name, B, layout, steps, warmup, world, rotate_gib, seed, spinup_ms=300.0, streams=1,
             sync_every=0, graph=False, extra_streams=()):
-    """Time `steps` launches of `kernel` over batches of B resident configurations.
-    Returns a dict (wall, kernel_ms_avg, bytes, sets) plus the graph-replay figures if asked."""
+    """Time `steps` launches of `kernel` over batches of B resident configurations (steps=None:
+    a budget of ~SIDE_TARGET_MS of launches, budget_steps).  Returns a dict (wall,
+    kernel_ms_avg, bytes, sets, steps) plus the graph-replay figures if asked."""
     ds = DT[dt_name]
     es = 4 if dt_name == "f32" else 8
     ns = nsets_for(mb.n, B, es, kernel, rotate_gib)
     sets = make_sets(mb, B, ds, kernel, ns, seed, layout=layout)
     launch = batch_launcher(mb, sets, kernel, ds, layout, B)
+    if steps is None:
+        steps = budget_steps(launch)
     wall, km = time_launches(launch, steps, warmup, world, spinup_ms, streams, sync_every)
-    r = {"wall": wall, "kernel_ms_avg": km, "bytes": set_bytes(mb.n, B, es, kernel), "sets": ns}
+    r = {"wall": wall, "kernel_ms_avg": km, "bytes": set_bytes(mb.n, B, es, kernel), "sets": ns, "steps": steps}
     if graph:
         gw, gkm, gl = time_graph(launch, steps)
         r.update({"graph_wall": gw, "graph_kernel_ms_avg": gkm, "graph_launches": gl})
@@ -378,17 +394,40 @@ def measure(mb, kernel, dt_name, B, layout, steps, warmup, world, rotate_gib, se
     return r
 
 
+def layout_ab(mb, kernel, dt_name, B, rounds=5, seed=chains.SEED + 5):
+    """The same kernel on SoA rows and on the tiled layout, interleaved round by round in one
+    process (each round ~SIDE_TARGET_MS / 2 of launches per layout): per-launch medians."""
+    ds = DT[dt_name]
+    es = 4 if dt_name == "f32" else 8
+    ns = nsets_for(mb.n, B, es, kernel, 1.25)
+    launches = {lay: batch_launcher(mb, make_sets(mb, B, ds, kernel, ns, seed, layout=lay), kernel, ds, lay, B)
+                for lay in ("soa", "tiled")}
+    steps = budget_steps(launches["soa"], SIDE_TARGET_MS / 2)
+    res = {lay: [] for lay in launches}
+    for r in range(rounds):
+        for lay, launch in launches.items():
+            res[lay].append(time_launches(launch, steps, 5, 1, 100.0 if r == 0 else 0.0)[1] * 1e3)
+    del launches
+    torch.cuda.empty_cache()
+    out = {f"{lay}_us_median": float(np.median(v)) for lay, v in res.items()}
+    out.update({f"{lay}_us_rounds": [round(x, 3) for x in v] for lay, v in res.items()})
+    out.update({"launches_per_round": steps, "rounds": rounds, "batch": B, "dtype": dt_name,
+                "note": "interleaved in one process: soa then tiled, every round"})
+    return out
+
+
 def side_workloads(mb7, a):
     """Secondary measurements (one GPU, serial launches): the other SURVEY §8(d) configs."""
     sec = {}
-    steps = max(20, a.steps // 4)
 
     def one(name, mb, kernel, dt_name, B=a.batch, layout=a.layout, graph=False, streams=(1,)):
-        r = measure(mb, kernel, dt_name, B, layout, steps, 5, 1, a.rotate_gib, chains.SEED + 31, graph=graph,
+        r = measure(mb, kernel, dt_name, B, layout, None, 5, 1, a.rotate_gib, chains.SEED + 31, graph=graph,
                     extra_streams=streams[1:])
-        sec[name] = {"evals_per_s": B * steps / r["wall"], "kernel_ms_avg": r["kernel_ms_avg"], "batch": B,
+        sec[name] = {"evals_per_s": B * r["steps"] / r["wall"], "kernel_ms_avg": r["kernel_ms_avg"], "batch": B,
+                     "launches": r["steps"],
                      "layout": layout, "dtype": dt_name, "hbm_frac": r["bytes"] / (r["kernel_ms_avg"] * 1e-3) / HBM_PEAK,
-                     "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64") for k in kernel.split("_"))}
+                     "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64", B, layout == "tiled")
+                                             for k in kernel.split("_"))}
         if graph:  # the same launches replayed from a HIP graph; rates over the launches replayed
             gl = r["graph_launches"]
             sec[name + "_graph"] = {"evals_per_s": B * gl / r["graph_wall"],
@@ -416,10 +455,13 @@ def side_workloads(mb7, a):
     one("rnea_float14_tree_f32", mbt, "rnea", "f32")
     one("fd_float14_tree_f32", mbt, "fd", "f32")
     # fused rollout: K forward-dynamics + Euler steps per launch
-    K, nl = 16, 40
+    K = 16
     for dn, dt in (("f32", torch.float32), ("f64", torch.float64)):
-        w, km = time_launches(rollout_launcher(mb7, a.batch, dt, K), nl, 3, 1, 300.0)
+        rl = rollout_launcher(mb7, a.batch, dt, K)
+        nl = budget_steps(rl, lo=100)
+        w, km = time_launches(rl, nl, 3, 1, 300.0)
         sec[f"rollout_fr3_{dn}_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
+                                        "launches": nl,
                                         "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", dn == "f64"),
                                         "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)"}
     return sec
@@ -456,6 +498,33 @@ def host_cores():
         return os.cpu_count() or 1
 
 
+def cpu_share(cgroup_root="/sys/fs/cgroup"):
+    """(cores, how): the host cores this process may use, read at run time -- the cgroup CPU
+    quota when one is set (v2 cpu.max, or v1 cpu.cfs_quota_us / cpu.cfs_period_us), capped by
+    the affinity set; otherwise the affinity set itself."""
+    visible = host_cores()
+    quota = None
+    try:
+        with open(os.path.join(cgroup_root, "cpu.max")) as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = (int(q) / int(period), f"cgroup v2 cpu.max = {q} {period}")
+    except (OSError, ValueError):
+        try:
+            with open(os.path.join(cgroup_root, "cpu", "cpu.cfs_quota_us")) as f:
+                q = int(f.read())
+            with open(os.path.join(cgroup_root, "cpu", "cpu.cfs_period_us")) as f:
+                period = int(f.read())
+            if q > 0:
+                quota = (q / period, f"cgroup v1 cfs quota {q} / period {period}")
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        cores = max(1, min(visible, int(quota[0])))
+        return cores, f"{quota[1]} -> {quota[0]:.2f} CPUs, affinity set {visible}"
+    return visible, f"no cgroup CPU quota; affinity set of {visible} CPUs"
+
+
 def cpu_baseline(n, kernel, cpu_seconds):
     """fp64 CPU restatement (oracle/, kind "port") timed on this host's cores."""
     from oracle import oracle, urdf_model
@@ -465,8 +534,7 @@ def cpu_baseline(n, kernel, cpu_seconds):
     raw = urdf_model.model_raw_from_urdf(xml)
     om = oracle.Model(raw)
     visible = host_cores()
-    # the GPU box's CPU share is 16 (os.cpu_count() there shows the whole machine)
-    cores = max(1, min(16, visible))
+    cores, how = cpu_share()
     mbl = ([l["lower"] for l in raw["limits"]], [l["upper"] for l in raw["limits"]],
            [l["velocity"] for l in raw["limits"]], [l["effort"] for l in raw["limits"]])
     kinds = ("q", "qd", "tau") if kernel == "fd" else ("q", "qd", "qdd")
@@ -493,12 +561,13 @@ def cpu_baseline(n, kernel, cpu_seconds):
     call(*x, nthreads=cores)
     dt = time.perf_counter() - t
     return {"value": sample / dt, "unit": "evals/s", "cores": cores, "kind": "port",
-            "host_cpus_visible": visible, "nproc": os.cpu_count(),
+            "cores_source": how, "host_cpus_visible": visible, "nproc": os.cpu_count(),
             "single_thread_evals_per_s": rate1, "single_thread_us_per_call": 1e6 / rate1,
             "single_thread_crba_us_per_call": 1e6 / crba1,
             "sample": f"{sample} {'fr3' if n == 7 else f'chain{n}'} configs (same distributions/seed as the GPU run), "
-                      f"fp64 oracle {kernel} over {cores} OpenMP threads (of {visible} visible CPUs, cap 16 = the "
-                      f"GPU box's CPU share), {dt:.2f} s wall; single-thread {rate1:.3g} evals/s"}
+                      f"fp64 oracle {kernel} over {cores} OpenMP threads ({how}), {dt:.2f} s wall; "
+                      f"single-thread {rate1:.3g} evals/s (the reference's one-call-per-configuration use, "
+                      f"main.cpp:69)"}
 
 
 def load_traffic(workload):
@@ -533,7 +602,7 @@ def main(a):
     else:
         r = measure(mb, a.kernel, a.dtype, B, a.layout, a.steps, a.warmup, world, a.rotate_gib, seed, a.spinup_ms,
                     a.streams, a.sync_every)
-        kpath = "+".join(mb.kernel_path(k, a.dtype == "f64") for k in a.kernel.split("_"))
+        kpath = "+".join(mb.kernel_path(k, a.dtype == "f64", B, a.layout == "tiled") for k in a.kernel.split("_"))
     wall, kern_ms = rdist.max_over_ranks([r["wall"], r["kernel_ms_avg"]], world, dev)
     value = global_batch * a.steps / wall
     bytes_per_eval = set_bytes(n, 1, esize, a.kernel)
@@ -583,21 +652,14 @@ def main(a):
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.stub:
         line["cpu_baseline"] = cpu_baseline(n, a.kernel, a.cpu_seconds)
     if rank == 0 and not a.no_secondary and world == 1 and n == 7 and not a.stub:
-        steps = a.steps
-        r2 = measure(mb, a.kernel, a.dtype, a.batch, a.layout, steps, 5, 1, a.rotate_gib, seed, 50.0, 2)
+        r2 = measure(mb, a.kernel, a.dtype, a.batch, a.layout, None, 5, 1, a.rotate_gib, seed, 50.0, 2)
         sec[f"{a.kernel}_{a.dtype}_{a.layout}_2streams"] = {
-            "evals_per_s": a.batch * steps / r2["wall"], "step_ms_device": r2["kernel_ms_avg"],
-            "hbm_frac_effective": r2["bytes"] / (r2["kernel_ms_avg"] * 1e-3) / HBM_PEAK}
-        # the comparable SoA line (north_star's layout) and the reduced-precision fp32 variant
-        other = "f32" if a.dtype == "f64" else "f64"
-        for dt_name, layout in ((a.dtype, "soa"), (other, a.layout), (other, "soa")):
-            if layout == a.layout and dt_name == a.dtype:
-                continue
-            rr = measure(mb, a.kernel, dt_name, a.batch, layout, steps, 5, 1, a.rotate_gib, seed + 7, 100.0)
-            sec[workload_name(a.kernel, n, dt_name, layout, a.batch)] = {
-                "evals_per_s": a.batch * steps / rr["wall"], "kernel_ms_avg": rr["kernel_ms_avg"],
-                "hbm_frac": rr["bytes"] / (rr["kernel_ms_avg"] * 1e-3) / HBM_PEAK, "dtype": dt_name,
-                "layout": layout, "note": "reduced precision (the reference computes in f64)" if dt_name == "f32" else ""}
+            "evals_per_s": a.batch * r2["steps"] / r2["wall"], "step_ms_device": r2["kernel_ms_avg"],
+            "launches": r2["steps"], "hbm_frac_effective": r2["bytes"] / (r2["kernel_ms_avg"] * 1e-3) / HBM_PEAK}
+        # SoA rows (north_star's layout) against the tiled layout, interleaved in this process,
+        # for the headline kernel in both precisions and for forward dynamics in fp64
+        for kern, dt_name in ((a.kernel, "f64"), (a.kernel, "f32"), ("fd", "f64")):
+            sec[f"layout_ab_{kern}_{dt_name}"] = layout_ab(mb, kern, dt_name, a.batch)
         sec.update(side_workloads(mb, a))
         sec["single_call"] = single_call()
         if "cpu_baseline" in line:

@@ -8,8 +8,11 @@
  *   multibody_rnea_batch_*     <- multibody_rnea      (lib.rs:15-30, multibody.rs:111-153)
  *   multibody_fd_batch_*       <- no reference entry point: forward dynamics defined as
  *                                 qdd = sym(H)^-1 (tau - rnea(q,qd,0)) with H from
- *                                 multibody_crba (multibody.rs:155-174), computed by the
- *                                 Articulated-Body Algorithm
+ *                                 multibody_crba (multibody.rs:155-174) (SURVEY.md §8(a)
+ *                                 A10), computed by exactly that definition fused per
+ *                                 configuration (RNEA bias + CRBA + L D L^T) for serial chains
+ *                                 up to 8 links, by the Articulated-Body Algorithm otherwise
+ *                                 (rb_set_tuning "fd_form")
  *   multibody_rollout_batch_*  <- K fused forward-dynamics + semi-implicit Euler steps
  *                                 (MPC shooting)
  *   multibody_crba_batch_*     <- multibody_crba      (lib.rs:32-43)
@@ -105,10 +108,13 @@ int multibody_topology(const Multibody *mb, int *parent, int *joint_type);
  * the first batched call); call before capturing batched calls into a hipGraph. */
 int multibody_upload(const Multibody *mb);
 
-/* Which kernel runs for this model on the current device; kind 0 = rnea, 1 = fd,
- * 2 = crba, 3 = rollout, 4 = fwd_kin, 5 = jac.  1 = model-specialised kernel compiled at
- * first use by hipRTC, 0 = precompiled generic kernel (also when hipRTC failed;
- * rb_last_error() holds the log -- a tree model's calls then fail with RB_ERR_UNSUPPORTED). */
+/* Which kernel a launch of `batch` configurations (tiled != 0: the *_tiled entry points)
+ * runs for this model on the current device; kind 0 = rnea, 1 = fd, 2 = crba, 3 = rollout,
+ * 4 = fwd_kin, 5 = jac.  1 = model-specialised kernel compiled at first use by hipRTC (this
+ * call compiles exactly the form such a launch takes), 0 = precompiled generic kernel (also
+ * when hipRTC failed; rb_last_error() holds the log -- a tree model's calls then fail with
+ * RB_ERR_UNSUPPORTED).  multibody_kernel_path = a 2^20-configuration SoA launch. */
+int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled);
 int multibody_kernel_path(const Multibody *mb, int kind, int f64);
 int multibody_rnea_kernel_path(const Multibody *mb, int f64);
 /* Where the reference's single-configuration queries (rigidbody.h: rnea, crba, fwd_kin,
@@ -116,8 +122,9 @@ int multibody_rnea_kernel_path(const Multibody *mb, int f64);
  * the host; serial revolute chains of a precompiled DOF on an FMA3/AVX2 CPU), 1 = one GPU
  * launch per call (trees / prismatic joints, or rb_set_tuning("single_gpu", 1)). */
 int multibody_single_config_path(const Multibody *mb);
-/* The generated source of a model-specialised kernel (returns its length; copies at
- * most cap-1 bytes + NUL into buf when buf != NULL). */
+/* The generated source of a model-specialised kernel in its large-batch SoA form (the
+ * lane form of a 2^20-configuration SoA launch; returns its length; copies at most cap-1
+ * bytes + NUL into buf when buf != NULL). */
 int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap);
 /* hipRTC-compiles that kernel for `arch` (NULL = "gfx950") without a device; returns
  * the code-object size, or minus an rb_status code (log in rb_last_error()). */
@@ -129,12 +136,6 @@ const char *rb_version(void);
 /* Launch-shape knobs for A/B measurements (keys and defaults: INTEGRATION.md "Knobs",
  * rigidbody-rs_amd/csrc/tuning.hpp); defaults are the tuned values.  Process-wide. */
 int rb_set_tuning(const char *key, int value);
-/* Bandwidth probe with the batched kernels' access pattern: reads rows_in SoA rows and
- * writes rows_out rows of `batch` floats (width 1/2/4: 4/8/16 B per lane; + 16 * nt with
- * nt bit 0 = non-temporal loads, bit 1 = non-temporal stores, bit 2 = tiled layout: element
- * (row r, config b) at ((b / 256) * rows + r) * 256 + b % 256, batch a multiple of 256). */
-int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
-                      int width, void *stream);
 
 /* ---- batched device-pointer entry points (asynchronous on `stream`) ------------ */
 int multibody_rnea_batch_f32(const Multibody *mb, const float *q, const float *qd,
@@ -169,7 +170,8 @@ int rb_from_tiled_f32(const float *src, float *dst, int64_t ld, int rows, int64_
 int rb_from_tiled_f64(const double *src, double *dst, int64_t ld, int rows, int64_t batch, void *stream);
 
 /* Fused rollout for MPC shooting: K steps of semi-implicit Euler on the forward dynamics
- * above, qd += dt * qdd(q, qd, tau_k); q += dt * qd, state kept in registers.  q and qd
+ * above (Articulated-Body form), qd += dt * qdd(q, qd, tau_k); q += dt * qd, the state
+ * kept on chip between steps (LDS for fp32 chains up to 16 links, registers otherwise).  q and qd
  * ([n][ld]) are read and overwritten with the final state; tau_seq is [K][n][ld] (step k,
  * joint j, config b at (k*n + j)*ld + b); traj (same shape, may be NULL) receives q after
  * every step. */

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <map>
 #include <mutex>
@@ -84,13 +85,16 @@ struct Multibody {
     // model-specialised hipRTC kernels, keyed by (device, kind, dtype, trig, tuning tag, form)
     mutable std::map<std::string, rbamd::JitKernel> jit;
     mutable std::map<std::string, int> jit_device;
-    // per-launch fast path of jit_get: [device][kind][f64][fast trig][requested pack] -> the
-    // kernel resolved under tuning generation `gen` (map nodes never move or die before free)
-    struct JitSlot {
-        std::atomic<unsigned> gen{0};
-        std::atomic<const rbamd::JitKernel *> jk{nullptr};
+    // per-launch fast path of jit_get: [device][kind][f64][fast trig][requested pack][tail] ->
+    // the kernel resolved under one tuning generation, published as ONE pointer to an
+    // immutable {gen, kernel} record (records live in jit_pub and never move or die before
+    // free), so a reader never pairs a generation with another generation's kernel
+    struct JitPub {
+        unsigned gen;
+        const rbamd::JitKernel *jk;
     };
-    mutable JitSlot jit_fast[16][6][2][2][4][2];  // last index: sequential-pair RNEA tail on
+    mutable std::deque<JitPub> jit_pub;
+    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][4][2] = {};
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
@@ -177,12 +181,13 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
     const bool fst = fast && !f64;
     const unsigned gen = rbamd::tuning_generation();
-    Multibody::JitSlot *slot = nullptr;
+    std::atomic<const Multibody::JitPub *> *slot = nullptr;
     if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 4) {
         slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][tail > 0 ? 1 : 0];
-        if (slot->gen.load(std::memory_order_acquire) == gen) return slot->jk.load(std::memory_order_relaxed);
+        if (const Multibody::JitPub *p = slot->load(std::memory_order_acquire))
+            if (p->gen == gen) return p->jk;
     }
-    if (pack <= 0) pack = rbamd::jit_pack(kind, f64, mb->model.n);
+    if (pack <= 0) pack = rbamd::jit_model_pack(mb->model, kind, f64, 0);
     if (!(kind == rbamd::JitKind::Rnea && pack == 3)) tail = 0;
     const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
                             (fst ? ":fast" : ":precise") + rbamd::jit_tag(kind, f64, mb->model.n) + ":q" +
@@ -194,9 +199,11 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
         mb->jit_device[key] = d;
     }
     const rbamd::JitKernel *res = it->second.function ? &it->second : nullptr;
-    if (slot) {
-        slot->jk.store(res, std::memory_order_relaxed);
-        slot->gen.store(gen, std::memory_order_release);
+    // publish only if the tuning did not change while this call resolved the kernel (the
+    // key above was built from the tuning state of generation `gen` or a later one)
+    if (slot && rbamd::tuning_generation() == gen) {
+        mb->jit_pub.push_back(Multibody::JitPub{gen, res});
+        slot->store(&mb->jit_pub.back(), std::memory_order_release);
     }
     return res;
 }
@@ -728,18 +735,32 @@ int multibody_topology(const Multibody *mb, int *parent, int *joint_type) {
     return RB_OK;
 }
 
-int multibody_kernel_path(const Multibody *mb, int kind, int f64) {
+int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled) {
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
     if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
+    if (batch < 1) return -set_err(RB_ERR_ARG, "batch must be positive");
     if (kind >= 4 && (!f64 || mb->model.serial_revolute())) return 0;  // precompiled fp64 kinematics
     if (!rbamd::jit_enabled()) return 0;
-    if (jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 || kind >= 4 ? false : fast_trig())) return 1;
-    int d = 0;
-    (void)hipGetDevice(&d);
+    // the same kernel resolution as the launchers (launch_*_any) for a launch of `batch`
+    const uint32_t B = batch < kChunk ? (uint32_t)batch : (uint32_t)kChunk;
+    const rbamd::JitKernel *jk = nullptr;
+    if (kind == 0) {
+        jk = jit_rnea(mb, f64 != 0, fast_trig(), B, tiled != 0);
+    } else if (kind == 1) {
+        const int pack = (rbamd::tuning().pack < 0 && B < kPackMinBatch) ? 1 : 0;
+        jk = jit_get(mb, rbamd::JitKind::Fd, f64 != 0, fast_trig(), pack);
+    } else {
+        jk = jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 || kind >= 4 ? false : fast_trig());
+    }
+    if (jk) return 1;
     std::lock_guard<std::mutex> lk(mb->mu);
     for (auto &kv : mb->jit)
         if (!kv.second.error.empty()) g_last_error = kv.second.error;
     return 0;
+}
+
+int multibody_kernel_path(const Multibody *mb, int kind, int f64) {
+    return multibody_kernel_path_ex(mb, kind, f64, int64_t(1) << 20, 0);
 }
 
 int multibody_rnea_kernel_path(const Multibody *mb, int f64) { return multibody_kernel_path(mb, 0, f64); }
@@ -785,15 +806,6 @@ int multibody_upload(const Multibody *mb) {
 void multibody_result_free(double *p) { std::free(p); }
 const char *rb_last_error(void) { return g_last_error.c_str(); }
 const char *rb_version(void) { return RB_VERSION; }
-
-int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
-                      int width, void *stream) {
-    if (!in || !out) return set_err(RB_ERR_NULL, "NULL array");
-    if (rows_in < 1 || rows_out < 0 || batch < 0 || ld < batch || batch > kChunk || ((width & 15) != 1 && (width & 15) != 2 && (width & 15) != 4) || (width >> 4) > 7)
-        return set_err(RB_ERR_ARG, "bad probe shape");
-    hipError_t e = rbamd::launch_probe_rows(in, out, rows_in, rows_out, (uint32_t)batch, ld, width, (hipStream_t)stream);
-    return e == hipSuccess ? RB_OK : hip_err(e, "probe launch");
-}
 
 }  // extern "C"
 

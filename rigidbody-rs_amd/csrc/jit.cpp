@@ -3,6 +3,7 @@
 
 #include <hip/hiprtc.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -344,8 +345,8 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     // RB_JIT_DUMP=dir: keep every compiled source and code object for inspection
     // (llvm-objdump / llvm-readelf on the .co: registers, scratch, ISA of what really runs)
     if (const char *dir = std::getenv("RB_JIT_DUMP")) {
-        static int seq = 0;
-        const std::string base = std::string(dir) + "/jit_" + std::to_string(seq++) + "_k" +
+        static std::atomic<int> seq{0};
+        const std::string base = std::string(dir) + "/jit_" + std::to_string(seq.fetch_add(1)) + "_k" +
                                  std::to_string((int)kind) + (f64 ? "_f64" : "_f32") + "_p" + std::to_string(pack);
         if (FILE *f = std::fopen((base + ".hip").c_str(), "wb")) {
             std::fwrite(src.data(), 1, src.size(), f);

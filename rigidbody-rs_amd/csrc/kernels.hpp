@@ -56,8 +56,4 @@ template <typename T>
 hipError_t launch_fill_uniform(T *x, int rows, uint32_t B, int64_t ld, const double *lohi_dev,
                                uint64_t seed, hipStream_t s);
 
-// Bandwidth probe (probe.hip): width 1 = 4 B per lane, 4 = 16 B per lane.
-hipError_t launch_probe_rows(const float *in, float *out, int rows_in, int rows_out, uint32_t B, int64_t ld,
-                             int width, hipStream_t s);
-
 }  // namespace rbamd

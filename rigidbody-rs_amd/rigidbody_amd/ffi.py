@@ -84,6 +84,7 @@ _sig("multibody_rnea_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i
 _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
 _sig("multibody_single_config_path", ctypes.c_int, [_vp])
 _sig("multibody_kernel_path", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int])
+_sig("multibody_kernel_path_ex", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _i64, ctypes.c_int])
 _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
 KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3, "fwd_kin": 4, "jac": 5}
@@ -94,7 +95,6 @@ for _t in ("f32", "f64"):
     _sig(f"multibody_rollout_batch_{_t}", ctypes.c_int,
          [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_int, _vp, _i64, _i64, _vp])
 _sig("rb_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
-_sig("rb_probe_rows_f32", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _i64, _i64, ctypes.c_int, _vp])
 _sig("multibody_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
 for _t in ("f32", "f64"):
     _sig(f"multibody_rnea_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp])
@@ -300,9 +300,10 @@ class Multibody:
     def upload(self):
         _check(_lib.multibody_upload(self._h), "upload")
 
-    def kernel_path(self, kind="rnea", f64=False) -> str:
-        """'jit' if the model-specialised hipRTC kernel of `kind` runs on this device."""
-        r = _lib.multibody_kernel_path(self._h, KINDS[kind], int(bool(f64)))
+    def kernel_path(self, kind="rnea", f64=False, batch=1 << 20, tiled=False) -> str:
+        """'jit' if the model-specialised hipRTC kernel of `kind` runs on this device for a
+        launch of `batch` configurations (tiled: the *_tiled entry points)."""
+        r = _lib.multibody_kernel_path_ex(self._h, KINDS[kind], int(bool(f64)), int(batch), int(bool(tiled)))
         if r < 0:
             raise RigidBodyError(last_error())
         return "jit" if r == 1 else "generic"

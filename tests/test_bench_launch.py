@@ -55,3 +55,24 @@ def test_failed_rank_fails_the_job():
                         "--steps", "1"], capture_output=True, text=True, timeout=300, env=e)
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_cpu_share_reads_the_cgroup_quota(tmp_path):
+    """cpu_baseline's core count comes from the cgroup CPU quota when one is set (v2
+    cpu.max, v1 cfs quota/period), capped by the affinity set, else the affinity set."""
+    import bench
+
+    vis = bench.host_cores()
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    cores, how = bench.cpu_share(str(tmp_path))
+    assert cores == min(16, vis) and "cpu.max" in how
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    cores, how = bench.cpu_share(str(tmp_path))
+    assert cores == vis and "affinity" in how
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("250000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert bench.cpu_share(str(v1))[0] == min(2, vis)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
+    assert bench.cpu_share(str(v1))[0] == vis

@@ -102,3 +102,24 @@ def test_single_config_path_reporting(ffi):
     finally:
         ffi.set_tuning("single_gpu", 0)
     assert mb.single_config_path() == "host"
+
+
+@pytest.mark.parametrize("n", [7, 12])
+def test_general_axis_chains_on_host(n, ffi):
+    """General-axis serial chains (RB_MODEL_GENERAL_AXES | RB_MODEL_URDF_TREE, SURVEY §8(f)
+    rank 4) run the single-configuration ABI on the host too: the packer's per-link frame
+    change plus the kTailOut rotation that fwd_kin / jac start from, against the oracle's
+    general-axis reading (itself pinned to the 6x6 formulation, tests/test_general.py)."""
+    from oracle import oracle, urdf_model
+    from rigidbody_amd import chains
+
+    xml = chains.general_chain_urdf(n)
+    mb = ffi.Multibody.from_urdf_string(xml, ffi.URDF_TREE | ffi.GENERAL_AXES)
+    assert mb.single_config_path() == "host"
+    om = oracle.Model(frames=urdf_model.model_frames_from_urdf_tree(xml), general=True)
+    rng = np.random.default_rng(n)
+    for _ in range(8):
+        q, qd, qdd = (rng.uniform(-2, 2, n) for _ in range(3))
+        for got, want in ((mb.rnea(q, qd, qdd), om.rnea(q, qd, qdd)), (mb.crba_raw(q), om.crba_raw(q)),
+                          (mb.fwd_kin(q), om.fwd_kin(q)), (mb.jac_raw(q), om.jac_raw(q))):
+            assert np.abs(got - want).max() <= 1e-11 * (1 + np.abs(want).max()), n

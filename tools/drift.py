@@ -19,6 +19,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "rigidbody-rs_amd")]
 import bench  # noqa: E402
 from rigidbody_amd import ffi  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import probe_lib  # noqa: E402
+
+plib = probe_lib.lib()
 
 
 def series(launch, n, chunk=100):
@@ -72,7 +76,7 @@ def main():
     pargs = [(i.data_ptr(), o.data_ptr(), 21, 7, B, B, 1 + 16 * 7, sp) for i, o in pin]
 
     def probe(k):
-        if lib.rb_probe_rows_f32(*pargs[k % nsets]):
+        if plib.rb_probe_rows_f32(*pargs[k % nsets]):
             raise RuntimeError(ffi.last_error())
 
     def rnea(k):

@@ -3,15 +3,18 @@
 // can reach with a given per-lane access width: 4 B (one fp32 configuration per lane, what
 // the kernels do), 8 B or 16 B (two / four consecutive configurations per lane).  Also used to calibrate
 // rocprofv3 FETCH_SIZE / WRITE_SIZE against a known byte count.
+//
+// Measurement tooling, not product: built on its own as tools/microbench/libprobe.so
+// (`make -C tools/microbench`), loaded by tools/probe_lib.py.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
-#include "dofs.hpp"
-#include "kernels.hpp"
-
 namespace rbamd {
 namespace dev {
+
+constexpr int kBlock = 256;
+inline unsigned grid_for(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 
 template <int W>
 struct VecOf;
@@ -111,3 +114,16 @@ hipError_t launch_probe_rows(const float *in, float *out, int rows_in, int rows_
 }
 
 }  // namespace rbamd
+
+// Reads rows_in rows and writes rows_out rows of `batch` floats (width 1/2/4: 4/8/16 B per
+// lane; + 16 * nt with nt bit 0 = non-temporal loads, bit 1 = non-temporal stores, bit 2 =
+// tiled layout: element (row r, config b) at ((b / 256) * rows + r) * 256 + b % 256, batch a
+// multiple of 256).  Returns a hipError_t code (0 = success).
+extern "C" int rb_probe_rows_f32(const float *in, float *out, int rows_in, int rows_out, int64_t batch, int64_t ld,
+                                 int width, void *stream) {
+    if (!in || !out || rows_in < 1 || rows_out < 0 || batch < 0 || ld < batch || batch >= (int64_t(1) << 28))
+        return (int)hipErrorInvalidValue;
+    const int w = width & 15;
+    if ((w != 1 && w != 2 && w != 4) || (width >> 4) > 7) return (int)hipErrorInvalidValue;
+    return (int)rbamd::launch_probe_rows(in, out, rows_in, rows_out, (uint32_t)batch, ld, width, (hipStream_t)stream);
+}

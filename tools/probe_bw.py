@@ -12,6 +12,10 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "rigidbody-rs_amd")]
 from rigidbody_amd import ffi  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import probe_lib  # noqa: E402
+
+plib = probe_lib.lib()
 
 
 def run(rows_in, rows_out, width, nt=0, B=1 << 20, steps=100, rounds=5):
@@ -23,13 +27,13 @@ def run(rows_in, rows_out, width, nt=0, B=1 << 20, steps=100, rounds=5):
     sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     args = [(i.data_ptr(), o.data_ptr(), rows_in, rows_out, B, B, width + 16 * nt, sp) for i, o in sets]
     for k in range(200):
-        assert lib.rb_probe_rows_f32(*args[k % nsets]) == 0, ffi.last_error()
+        assert plib.rb_probe_rows_f32(*args[k % nsets]) == 0, ffi.last_error()
     ms = []
     for _ in range(rounds):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for k in range(steps):
-            lib.rb_probe_rows_f32(*args[k % nsets])
+            plib.rb_probe_rows_f32(*args[k % nsets])
         e1.record()
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1) / steps)

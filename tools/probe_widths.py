@@ -15,6 +15,10 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "rigidbody-rs_amd")]
 from rigidbody_amd import ffi  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import probe_lib  # noqa: E402
+
+plib = probe_lib.lib()
 
 
 def run(B, width, launches):
@@ -27,7 +31,7 @@ def run(B, width, launches):
 
     def go(k):
         i, o = bufs[k % nsets]
-        if lib.rb_probe_rows_f32(i.data_ptr(), o.data_ptr(), 21, 7, B, B, code, sp):
+        if plib.rb_probe_rows_f32(i.data_ptr(), o.data_ptr(), 21, 7, B, B, code, sp):
             raise RuntimeError(ffi.last_error())
 
     for k in range(20):

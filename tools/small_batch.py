@@ -23,6 +23,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "rigidbody-rs_amd")]
 import bench  # noqa: E402
 from rigidbody_amd import chains, ffi  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import probe_lib  # noqa: E402
+
+plib = probe_lib.lib()
 
 
 def probe_launcher(B, rows_in=21, rows_out=7, nt=7):
@@ -34,7 +38,7 @@ def probe_launcher(B, rows_in=21, rows_out=7, nt=7):
     args = [(i.data_ptr(), o.data_ptr(), rows_in, rows_out, B, B, 1 + 16 * nt) for i, o in sets]
 
     def launch(i, sp):
-        if lib.rb_probe_rows_f32(*args[i % nsets], sp):
+        if plib.rb_probe_rows_f32(*args[i % nsets], sp):
             raise RuntimeError(ffi.last_error())
 
     launch.keep = sets
