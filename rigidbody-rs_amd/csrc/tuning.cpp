@@ -28,7 +28,7 @@ bool tuning_experimental() {
 namespace {
 struct Key {
     const char *name;
-    int Tuning::*field;
+    std::atomic<int> Tuning::*field;
     bool experimental;
 };
 const Key kKeys[] = {
@@ -54,17 +54,15 @@ void from_env(Tuning &t) {
         if (k.experimental && !tuning_experimental()) continue;
         std::string var = "RB_";
         for (const char *c = k.name; *c; ++c) var += (char)(*c >= 'a' && *c <= 'z' ? *c - 32 : *c);
-        t.*(k.field) = env_int(var.c_str(), t.*(k.field));
+        (t.*(k.field)).store(env_int(var.c_str(), (t.*(k.field)).load()));
     }
 }
 }  // namespace
 
 Tuning &tuning() {
-    static Tuning t = [] {
-        Tuning x;
-        from_env(x);
-        return x;
-    }();
+    static Tuning t;
+    static const bool init = (from_env(t), true);
+    (void)init;
     return t;
 }
 
@@ -78,7 +76,7 @@ int tuning_set(const char *key, int value) {
     for (const Key &k : kKeys) {
         if (std::strcmp(k.name, key) != 0) continue;
         if (k.experimental && !tuning_experimental()) return 2;
-        tuning().*(k.field) = value;
+        (tuning().*(k.field)).store(value);
         g_generation.fetch_add(1, std::memory_order_acq_rel);
         return 0;
     }

@@ -7,61 +7,65 @@
 // caller cannot multiply the hipRTC kernel variants (jit.cpp cache key) or the test matrix.
 #pragma once
 
+#include <atomic>
+
 namespace rbamd {
 
+// Every knob is an atomic int: rb_set_tuning may run while other threads launch (a launch
+// reads each knob once; a concurrent change applies to the launches that read it after).
 struct Tuning {
     // ---- production
-    int jit = 1;  // 1: model-specialised hipRTC kernels where available (jit.hpp)
+    std::atomic<int> jit{1};  // 1: model-specialised hipRTC kernels where available (jit.hpp)
     // JIT fp32 forward dynamics: 2 = two configurations per lane on packed fp32
     // (spatial.hip.hpp f2; 512 configurations per 256-lane block), 1 = one per lane,
     // -1 auto (jit_pack in jit.cpp: chains up to 8 links, batches >= 2^18).
-    int pack = -1;
+    std::atomic<int> pack{-1};
     // Precompiled (generic) RNEA launch form: 1 grid-stride + register prefetch, 0 one
     // configuration per lane, -1 auto (streaming for fp64 and chains longer than 8 links,
     // where it measured 7-9% faster -- DESIGN.md §4).  The model-specialised kernels are
     // always one configuration per lane.
-    int rnea_stream = -1;
+    std::atomic<int> rnea_stream{-1};
     // Single-configuration ABI (multibody_rnea / _crba / _fwd_kin / _jac): 0 = on the calling
     // host thread with the lane bodies compiled for the host (host_eval.cpp) where the model
     // allows it, 1 = always a GPU launch (H2D, kernel, D2H, sync).
-    int single_gpu = 0;
+    std::atomic<int> single_gpu{0};
     // Forward dynamics algorithm of the model-specialised kernels: 1 = Articulated-Body
     // Algorithm (aba_body.hip.hpp), 2 = mass-matrix method (fdh_body.hip.hpp: bias torques by
     // RNEA, H by CRBA, L D L^T solve -- the oracle's own definition), -1 auto (jit.cpp
     // jit_fd_form: mass matrix for serial chains up to 8 links).
-    int fd_form = -1;
+    std::atomic<int> fd_form{-1};
 
     // ---- experimental (RB_EXPERIMENTAL=1)
-    int grid_factor = 1;  // streaming grid = grid_factor x resident blocks (capped by the batch)
+    std::atomic<int> grid_factor{1};  // streaming grid = grid_factor x resident blocks (capped by the batch)
     // JIT RNEA: bit 0 non-temporal loads, bit 1 non-temporal stores (every element is
     // touched once; measured -5% fp32 / -8% fp64 kernel time).
-    int rnea_nt = 3;
+    std::atomic<int> rnea_nt{3};
     // JIT forward dynamics / rollout: same bits as rnea_nt (-5% fp32 FD kernel time).
-    int fd_nt = 3;
+    std::atomic<int> fd_nt{3};
     // JIT kernels: amdgpu_waves_per_eu occupancy target; 0 compiler's choice, -1 auto
     // (4 for the fp32 rollout of chains up to 8 links: its K loop otherwise settles at
     // 129+ VGPRs, one wave per SIMD fewer; 361 vs 390 us for 16 FR3 steps).
-    int jit_waves = -1;
+    std::atomic<int> jit_waves{-1};
     // Model constants pinned per use (spatial.hip.hpp mconst): 1 on, 0 off, -1 auto = the
     // rollout of chains up to 16 links (fp32 337 vs 1736 us; fp64 810 vs 995 us); off for
     // forward dynamics (fp32 29.6 vs 31.9 us; fp64 71 vs 90 us; 30-link fp32 333 vs 1331 us)
     // and for the other kinds.
-    int opaque_consts = -1;
+    std::atomic<int> opaque_consts{-1};
     // JIT fp64 kernels: 1 = table-assisted sincos (spatial.hip.hpp sincos_tab), 0 = the
     // pi/2-reduction minimax sincos_cw, -1 auto (on).
-    int f64_tab = -1;
+    std::atomic<int> f64_tab{-1};
     // JIT ABA / CRBA: rotate symmetric inertia blocks as R_p (Rz S Rz^T) R_p^T with the double
     // angle (artinertia.hip.hpp to_parent_split); 0 = the folded E S E^T; -1 auto = on when
     // every joint frame R_p is a signed permutation.
-    int split_rot = -1;
+    std::atomic<int> split_rot{-1};
     // Free experiment selector, emitted as RB_VARIANT into every JIT source (A/B only).
-    int jit_variant = 0;
+    std::atomic<int> jit_variant{0};
     // Sequential-pair RNEA (pack 3): the last `seq_tail` percent of a launch's 256-configuration
     // tiles run one configuration per lane, so the blocks dispatched last carry half the
     // dependent chain (the launch's compute tail after its last rows land).  0 = all pairs,
     // -1 auto: 75 for the tiled layout (FR3 fp64 2^20: 40.5 vs 41.8 us), 0 for SoA (43.6-45.9 vs
     // 42.9 us), DESIGN.md §4.
-    int seq_tail = -1;
+    std::atomic<int> seq_tail{-1};
 };
 
 // Process-wide knobs, initialised from RB_JIT / RB_PACK / RB_RNEA_STREAM (and, with
