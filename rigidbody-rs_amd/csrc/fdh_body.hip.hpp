@@ -25,7 +25,7 @@ namespace rbamd {
 namespace dev {
 
 // Where the tau rows are loaded: 1 = after the bias sweep (default), 0 = with q and qd at the
-// start, 2 = after the mass matrix (jit_variant bits 0-1 = 1 / 2 select 0 / 2, A/B only).
+// start, 2 = after the factorisation (jit_variant bits 0-1 = 1 / 2 select 0 / 2, A/B only).
 // After the bias sweep the rows are not held across it (fp64: 121 instead of 134 VGPRs, 4
 // waves/SIMD instead of 3) and still land under the mass-matrix stage: FR3 2^20 tiled, fp64
 // 56.2 vs 57.0 us, fp32 paired 27.1 vs 28.1 us; at 65536 (fp32) 4.52 vs 4.63 us, while loading
@@ -34,36 +34,35 @@ namespace dev {
 #define RB_FDH_TAU_AT ((RB_VARIANT & 3) == 1 ? 0 : (RB_VARIANT & 3) == 2 ? 2 : 1)
 #endif
 
-template <typename T, int N, bool FAST, typename Tau, typename Out>
-RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&load_tau, Out &&out) {
-    T cs[N], sn[N], C[N], tv[N];
-    if constexpr (RB_FDH_TAU_AT == 0) load_tau(tv);
-    // 1. bias torques (multibody.rs:111-153 with ddq = 0)
-    {
-        V3<T> fn[N], ff[N];
-        RneaState<T> st;
-        rnea_fwd0<T, FAST>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0]);
+// 1. bias torques C = rnea(q, qd, 0) (multibody.rs:111-153 with ddq = 0); also the joint
+// (cos, sin) the later stages reuse.
+template <typename T, int N, bool FAST>
+RB_HD void fdh_bias(const T *mdl, const T (&qv)[N], const T (&qdv)[N], T (&cs)[N], T (&sn)[N], T (&C)[N]) {
+    V3<T> fn[N], ff[N];
+    RneaState<T> st;
+    rnea_fwd0<T, FAST>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0]);
 #pragma unroll
-        for (int j = 1; j < N; ++j) rnea_fwd<T, FAST>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j]);
-        reload_fence();
+    for (int j = 1; j < N; ++j) rnea_fwd<T, FAST>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j]);
+    reload_fence();
 #pragma unroll
-        for (int j = N - 1; j >= 1; --j) {
-            C[j] = fn[j].z;
-            rnea_bwd(mdl, j, cs[j], sn[j], ff[j], fn[j], ff[j - 1], fn[j - 1]);
-        }
-        C[0] = fn[0].z;
+    for (int j = N - 1; j >= 1; --j) {
+        C[j] = fn[j].z;
+        rnea_bwd(mdl, j, cs[j], sn[j], ff[j], fn[j], ff[j - 1], fn[j - 1]);
     }
-    if constexpr (RB_FDH_TAU_AT == 1) load_tau(tv);
-    // 2. joint-space inertia, upper triangle H[j][i] (j <= i) of the ABI's column-major matrix
-    T H[N][N];
+    C[0] = fn[0].z;
+}
+
+// 2.-3. the joint-space inertia H (crba_core, upper triangle H[j][i], j <= i, of the ABI's
+// column-major matrix) factored in place as H = L D L^T, root first: L[i][j] (i > j)
+// overwrites H[j][i]; Di = 1 / D.
+template <typename T, int N>
+RB_HD void fdh_factor(const T *mdl, const T (&cs)[N], const T (&sn)[N], T (&H)[N][N], T (&Di)[N]) {
     reload_fence();
     crba_core<T, N>(mdl, cs, sn, [&](int e, T v) {
         const int j = e % N, i = e / N;
         if (j <= i) H[j][i] = v;
     });
-    if constexpr (RB_FDH_TAU_AT >= 2) load_tau(tv);
-    // 3. H = L D L^T, root first: L[i][j] (i > j) overwrites H[j][i]; Di = 1 / D[j]
-    T D[N], Di[N];
+    T D[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         T w[N];  // w[k] = L[j][k] D[k]
@@ -83,7 +82,11 @@ RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&loa
             H[j][i] = s * Di[j];
         }
     }
-    // 4. L y = tau - C,  z = D^-1 y,  L^T x = z  (x = qdd)
+}
+
+// 4. L y = tau - C,  z = D^-1 y,  L^T x = z  (x = qdd); out(j, qdd_j), leaf first.
+template <typename T, int N, typename Out>
+RB_HD void fdh_solve(const T (&H)[N][N], const T (&Di)[N], const T (&tv)[N], const T (&C)[N], Out &&out) {
     T x[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -100,6 +103,22 @@ RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&loa
         x[i] = z;
         out(i, z);
     }
+}
+
+template <typename T, int N, bool FAST, typename Tau, typename Out>
+RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&load_tau, Out &&out) {
+    T cs[N], sn[N], C[N], tv[N];
+    if constexpr (RB_FDH_TAU_AT == 0) load_tau(tv);
+    fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C);
+    if constexpr (RB_FDH_TAU_AT == 1) load_tau(tv);
+    T H[N][N], Di[N];
+    if constexpr (RB_FDH_TAU_AT >= 2) {
+        fdh_factor<T, N>(mdl, cs, sn, H, Di);
+        load_tau(tv);
+    } else {
+        fdh_factor<T, N>(mdl, cs, sn, H, Di);
+    }
+    fdh_solve<T, N>(H, Di, tv, C, static_cast<Out &&>(out));
 }
 
 // Lane body: loads in first-use order (q, qd root->leaf, then tau), as aba_lane.
@@ -170,6 +189,64 @@ __device__ __forceinline__ void fdh_lane2(const f2 *mdl, const float *__restrict
             }
         },
         [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
+}
+
+// Wave-pair split for small batches (jit pack 4): at 65536 configurations the one-per-lane
+// grid is one wave per SIMD and the kernel time is the first rows' latency plus ONE wave's
+// dependent chain of ~1060 VALU instructions.  Here a 256-thread block covers 128
+// configurations (half a 256-configuration tile) with two wave pairs; in each pair the even
+// wave evaluates the bias torques (fdh_bias, ~45% of the work) and the odd wave, on another
+// SIMD (a block's waves go to different SIMDs), the mass matrix, its factorisation and --
+// after one block barrier that hands it the bias torques through LDS -- the solve.  Each
+// wave's chain is about half the fused one, on twice the waves.  The odd wave loads q and
+// tau, the even one q and qd (q twice: the second read is served by L2).
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void fdh_pair_block(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                               const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
+                                               int64_t ld, int64_t bs) {
+    __shared__ T shC[2][N][64];
+    const uint32_t w = threadIdx.x >> 6, g = w >> 1, l = threadIdx.x & 63u;
+    const uint32_t tile = blockIdx.x >> 1;
+    const uint32_t t = ((blockIdx.x & 1u) << 7) + (g << 6) + l;
+    const bool live = tile * 256u + t < B;
+    // lanes past B read the last configuration (always in this tile) and store nothing
+    const uint32_t off = (live ? t : (B - 1u) - tile * 256u) * (uint32_t)sizeof(T);
+    const int64_t o = (int64_t)tile * bs;
+    if ((w & 1u) == 0) {
+        T qv[N], qdv[N], cs[N], sn[N], C[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+            qdv[j] = ld_row(qd + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C);
+#pragma unroll
+        for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
+        __syncthreads();
+    } else {
+        T qv[N], tv[N], cs[N], sn[N], C[N], H[N][N], Di[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            tv[j] = ld_row(tau + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);
+        fdh_factor<T, N>(mdl, cs, sn, H, Di);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
+        fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) {
+            if (live) st_row(qdd + o, j * ld, off, v);
+        });
+    }
 }
 
 }  // namespace dev
