@@ -94,7 +94,7 @@ struct Multibody {
         const rbamd::JitKernel *jk;
     };
     mutable std::deque<JitPub> jit_pub;
-    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][5][2] = {};
+    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][4][2] = {};
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
@@ -182,7 +182,7 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     const bool fst = fast && !f64;
     const unsigned gen = rbamd::tuning_generation();
     std::atomic<const Multibody::JitPub *> *slot = nullptr;
-    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 5) {
+    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 4) {
         slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][tail > 0 ? 1 : 0];
         if (const Multibody::JitPub *p = slot->load(std::memory_order_acquire))
             if (p->gen == gen) return p->jk;
@@ -244,8 +244,7 @@ unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
         const unsigned P = (T - S) & ~1u;
         return P / 2u + (T - P);
     }
-    // pack 2 / 3: two configurations per lane; pack 4: the wave-pair split, 128 per block
-    const unsigned per_block = jk->pack == 4 ? 128u : 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
+    const unsigned per_block = 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
     return (unsigned)(((uint64_t)B + per_block - 1) / per_block);
 }
 

@@ -191,63 +191,5 @@ __device__ __forceinline__ void fdh_lane2(const f2 *mdl, const float *__restrict
         [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
 }
 
-// Wave-pair split for small batches (jit pack 4): at 65536 configurations the one-per-lane
-// grid is one wave per SIMD and the kernel time is the first rows' latency plus ONE wave's
-// dependent chain of ~1060 VALU instructions.  Here a 256-thread block covers 128
-// configurations (half a 256-configuration tile) with two wave pairs; in each pair the even
-// wave evaluates the bias torques (fdh_bias, ~45% of the work) and the odd wave, on another
-// SIMD (a block's waves go to different SIMDs), the mass matrix, its factorisation and --
-// after one block barrier that hands it the bias torques through LDS -- the solve.  Each
-// wave's chain is about half the fused one, on twice the waves.  The odd wave loads q and
-// tau, the even one q and qd (q twice: the second read is served by L2).
-template <typename T, int N, bool FAST>
-__device__ __forceinline__ void fdh_pair_block(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
-                                               const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
-                                               int64_t ld, int64_t bs) {
-    __shared__ T shC[2][N][64];
-    const uint32_t w = threadIdx.x >> 6, g = w >> 1, l = threadIdx.x & 63u;
-    const uint32_t tile = blockIdx.x >> 1;
-    const uint32_t t = ((blockIdx.x & 1u) << 7) + (g << 6) + l;
-    const bool live = tile * 256u + t < B;
-    // lanes past B read the last configuration (always in this tile) and store nothing
-    const uint32_t off = (live ? t : (B - 1u) - tile * 256u) * (uint32_t)sizeof(T);
-    const int64_t o = (int64_t)tile * bs;
-    if ((w & 1u) == 0) {
-        T qv[N], qdv[N], cs[N], sn[N], C[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            qv[j] = ld_row(q + o, j * ld, off);
-            __builtin_amdgcn_sched_barrier(0);
-            qdv[j] = ld_row(qd + o, j * ld, off);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C);
-#pragma unroll
-        for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
-        __syncthreads();
-    } else {
-        T qv[N], tv[N], cs[N], sn[N], C[N], H[N][N], Di[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            qv[j] = ld_row(q + o, j * ld, off);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            tv[j] = ld_row(tau + o, j * ld, off);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);
-        fdh_factor<T, N>(mdl, cs, sn, H, Di);
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
-        fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) {
-            if (live) st_row(qdd + o, j * ld, off, v);
-        });
-    }
-}
-
 }  // namespace dev
 }  // namespace rbamd

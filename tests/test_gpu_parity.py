@@ -671,9 +671,8 @@ def test_fd_forms_vs_oracle(dt, ffi, dev, fr3_text):
     1 = Articulated-Body Algorithm (aba_body.hip.hpp), 2 = the mass-matrix method
     (fdh_body.hip.hpp: rnea(q, qd, 0) bias, CRBA H, L D L^T solve -- the oracle's own
     definition, SURVEY §8(a) A10 over multibody.rs:111-174), fp32 with one and two
-    configurations per lane, and the mass-matrix form's wave-pair split (pack 4: bias torques
-    and mass matrix on two waves, joined through LDS), SoA and tiled, at B = 1, 255, 65536
-    (config 3) and the ragged 65539, against the oracle's CRBA solve:
+    configurations per lane, SoA and tiled, at B = 1, 255, 65536 (config 3) and the ragged
+    65539, against the oracle's CRBA solve:
       fp64: |qdd - qdd_oracle| <= 1e-9 max(1, cond(H)/1e3) (1 + |qdd|), torque residual 1e-8;
       fp32: the backward-error bound K <= 16 and the element-wise 1e-3 torque residual.
     SoA and tiled outputs of one kernel form are bit-identical."""
@@ -684,7 +683,7 @@ def test_fd_forms_vs_oracle(dt, ffi, dev, fr3_text):
     lim = mb.limits()
     dtype = torch.float64 if dt == "f64" else torch.float32
     npd = "float64" if dt == "f64" else "float32"
-    packs = (1, 4) if dt == "f64" else (1, 2, 4)
+    packs = (1,) if dt == "f64" else (1, 2)
     outs = {}
     try:
         for form in (1, 2):
