@@ -212,7 +212,11 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         "  const bool twoB = bA + 256u < B;\n"
         "  const uint32_t offB = offA + (uint32_t)bs * (uint32_t)sizeof(T);\n";
     std::string head_s = "extern \"C\" __global__ __launch_bounds__(256) ";
-    if (const int w = jit_waves(kind, f64, m.n))
+    // The paired mass-matrix FD fits 4 waves/SIMD at exactly 128 VGPRs with the occupancy
+    // target (130 and 3 waves without): FR3 2^20 tiled 26.4 vs 27.0 us.
+    int waves = jit_waves(kind, f64, m.n);
+    if (fdh && pack == 2 && tuning().jit_waves < 0) waves = 4;
+    if (const int w = waves)
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
     head_s += "void ";
     const char *head = head_s.c_str();

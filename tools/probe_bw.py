@@ -43,7 +43,10 @@ def run(rows_in, rows_out, width, nt=0, B=1 << 20, steps=100, rounds=5):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "tiled":
+    if len(sys.argv) > 1 and sys.argv[1] == "chain30":
+        # the 30-DOF RNEA shape (90 rows in / 30 out), SoA and tiled, with / without nt
+        out = [run(90, 30, 1, nt, B=1 << 20) for nt in (0, 3, 4, 7)]
+    elif len(sys.argv) > 1 and sys.argv[1] == "tiled":
         # SoA rows vs the tiled layout (nt bit 2), 4 B lanes, RNEA 7-DOF shape, three batch sizes
         out = [run(21, 7, 1, nt, B=B) for B in (1 << 20, 1 << 21, 1 << 22) for nt in (0, 3, 4, 7)]
     else:
