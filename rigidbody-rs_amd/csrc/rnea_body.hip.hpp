@@ -102,95 +102,10 @@ RB_HD void rnea_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
     out(0, fn[0].z);
 }
 
-// ---------------------------------------------------------- RNEA, reversible sweep
-// Long chains (rnea_any for N > kRevMinDof): the forward sweep keeps no per-link forces.
-// The backward sweep walks the kinematics back up the chain by the exact inverse of each
-// forward step (undo the joint terms, then w = E w', v = E v' + p x w, the same for a) and
-// forms f_j = I a + v x* I v there.  Per link only the joint inputs and (cos, sin) -- or,
-// with RECOMPUTE, q alone -- are held across the sweeps instead of the 6 force components
-// plus (cos, sin): 30 links fp32 from ~240 to ~120-150 VGPRs, for ~1/3 more VALU work.
-// The round trip of every link's velocity/acceleration costs a few ulp per link.
-template <typename T>
-RB_HD void rnea_kin_fwd(const Link<T> &L, T c, T s, T qd, T qdd, RneaState<T> &st) {
-    const M3<T> E = joint_rotation(L.Rp, c, s);
-    const V3<T> u = cross_sub(st.v, L.p, st.w);
-    const V3<T> ua = cross_sub(st.av, L.p, st.aw);
-    V3<T> wn = mul_t(E, st.w), vn = mul_t(E, u);
-    V3<T> awn = mul_t(E, st.aw), avn = mul_t(E, ua);
-    wn.z += qd;
-    awn.z += qdd;
-    avn.x = fmadd(vn.y, qd, avn.x);
-    avn.y = fmadd(-vn.x, qd, avn.y);
-    awn.x = fmadd(wn.y, qd, awn.x);
-    awn.y = fmadd(-wn.x, qd, awn.y);
-    st.w = wn; st.v = vn; st.aw = awn; st.av = avn;
-}
-
-// The exact inverse of rnea_kin_fwd: link j's state back to link j-1's.
-template <typename T>
-RB_HD void rnea_kin_inv(const Link<T> &L, T c, T s, T qd, T qdd, RneaState<T> &st) {
-    const M3<T> E = joint_rotation(L.Rp, c, s);
-    const V3<T> aw1 = v3(fmadd(-st.w.y, qd, st.aw.x), fmadd(st.w.x, qd, st.aw.y), st.aw.z - qdd);
-    const V3<T> av1 = v3(fmadd(-st.v.y, qd, st.av.x), fmadd(st.v.x, qd, st.av.y), st.av.z);
-    const V3<T> w1 = v3(st.w.x, st.w.y, st.w.z - qd);
-    const V3<T> w = mul(E, w1), aw = mul(E, aw1);
-    st.v = cross_add(mul(E, st.v), L.p, w);
-    st.av = cross_add(mul(E, av1), L.p, aw);
-    st.w = w;
-    st.aw = aw;
-}
-
-template <typename T, int N, bool FAST, bool RECOMPUTE, typename Out>
-RB_HD void rnea_eval_rev(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&qddv)[N], Out &&out) {
-    T cs[N], sn[N];
-    RneaState<T> st;
-    {
-        const Link<T> L0 = load_link(mdl, 0);
-        sin_cos<FAST>(qv[0], sn[0], cs[0]);
-        const M3<T> E = joint_rotation(L0.Rp, cs[0], sn[0]);
-        const T g = T(kGravity);
-        st.w = v3(T(0), T(0), qdv[0]);
-        st.v = v3(T(0), T(0), T(0));
-        st.aw = v3(T(0), T(0), qddv[0]);
-        st.av = v3(g * E.m[6], g * E.m[7], g * E.m[8]);  // E^T (0,0,g)
-    }
-#pragma unroll
-    for (int j = 1; j < N; ++j) {
-        sin_cos<FAST>(qv[j], sn[j], cs[j]);
-        rnea_kin_fwd(load_link(mdl, j), cs[j], sn[j], qdv[j], qddv[j], st);
-    }
-    reload_fence();
-    V3<T> gf = v3(T(0), T(0), T(0)), gn = v3(T(0), T(0), T(0));  // children's force, this frame
-#pragma unroll
-    for (int j = N - 1; j >= 0; --j) {
-        const Link<T> L = load_link(mdl, j);
-        V3<T> In, If, An, Af;
-        inertia_mul(L, st.w, st.v, In, If);
-        inertia_mul(L, st.aw, st.av, An, Af);
-        const V3<T> ff = cross_add(v3(Af.x + gf.x, Af.y + gf.y, Af.z + gf.z), st.w, If);
-        const V3<T> fn = cross_add(cross_add(v3(An.x + gn.x, An.y + gn.y, An.z + gn.z), st.w, In), st.v, If);
-        out(j, fn.z);  // multibody.rs:144
-        if (j > 0) {
-            T c = cs[j], s = sn[j];
-            if constexpr (RECOMPUTE) {
-                T qj = qv[j];
-                opaque(qj);  // a fresh evaluation, not the forward sweep's value kept alive
-                sin_cos<FAST>(qj, s, c);
-            }
-            gf = v3(T(0), T(0), T(0));
-            gn = v3(T(0), T(0), T(0));
-            rnea_bwd(mdl, j, c, s, ff, fn, gf, gn);
-            rnea_kin_inv(L, c, s, qdv[j], qddv[j], st);
-        }
-    }
-}
-
 template <typename T, int N, bool FAST, typename Topo, typename Out>
 RB_HD void rnea_any(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&qddv)[N],
                                          Out &&out) {
-    if constexpr (Topo::kSerial && (RB_VARIANT & 16) != 0)
-        rnea_eval_rev<T, N, FAST, (RB_VARIANT & 32) != 0>(mdl, qv, qdv, qddv, static_cast<Out &&>(out));
-    else if constexpr (Topo::kSerial)
+    if constexpr (Topo::kSerial)
         rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, static_cast<Out &&>(out));
     else
         rnea_eval_tree<T, N, FAST, Topo>(mdl, qv, qdv, qddv, static_cast<Out &&>(out));

@@ -303,19 +303,6 @@ __device__ __forceinline__ void st_row(T *__restrict__ base, int64_t row, uint32
     }
 }
 
-// Hides a value's provenance from the optimiser (no instruction): a recomputation from it
-// is not merged with an earlier identical one, so that one's result need not stay live.
-RB_HD void opaque(float &x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(x));
-#endif
-}
-RB_HD void opaque(double &x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(x));
-#endif
-}
-
 // Compiler-only fence: forces per-link constants to be re-read from LDS in a later
 // sweep instead of being kept live in VGPRs across the whole chain.
 RB_HD void reload_fence() { asm volatile("" ::: "memory"); }
