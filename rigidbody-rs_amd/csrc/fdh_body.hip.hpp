@@ -52,16 +52,9 @@ RB_HD void fdh_bias(const T *mdl, const T (&qv)[N], const T (&qdv)[N], T (&cs)[N
     C[0] = fn[0].z;
 }
 
-// 2.-3. the joint-space inertia H (crba_core, upper triangle H[j][i], j <= i, of the ABI's
-// column-major matrix) factored in place as H = L D L^T, root first: L[i][j] (i > j)
-// overwrites H[j][i]; Di = 1 / D.
+// 3. H = L D L^T in place, root first: L[i][j] (i > j) overwrites H[j][i]; Di = 1 / D.
 template <typename T, int N>
-RB_HD void fdh_factor(const T *mdl, const T (&cs)[N], const T (&sn)[N], T (&H)[N][N], T (&Di)[N]) {
-    reload_fence();
-    crba_core<T, N>(mdl, cs, sn, [&](int e, T v) {
-        const int j = e % N, i = e / N;
-        if (j <= i) H[j][i] = v;
-    });
+RB_HD void fdh_ldl(T (&H)[N][N], T (&Di)[N]) {
     T D[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -82,6 +75,18 @@ RB_HD void fdh_factor(const T *mdl, const T (&cs)[N], const T (&sn)[N], T (&H)[N
             H[j][i] = s * Di[j];
         }
     }
+}
+
+// 2.-3. the joint-space inertia H (crba_core, upper triangle H[j][i], j <= i, of the ABI's
+// column-major matrix), then its factorisation.
+template <typename T, int N>
+RB_HD void fdh_factor(const T *mdl, const T (&cs)[N], const T (&sn)[N], T (&H)[N][N], T (&Di)[N]) {
+    reload_fence();
+    crba_core<T, N>(mdl, cs, sn, [&](int e, T v) {
+        const int j = e % N, i = e / N;
+        if (j <= i) H[j][i] = v;
+    });
+    fdh_ldl<T, N>(H, Di);
 }
 
 // 4. L y = tau - C,  z = D^-1 y,  L^T x = z  (x = qdd); out(j, qdd_j), leaf first.
@@ -107,17 +112,12 @@ RB_HD void fdh_solve(const T (&H)[N][N], const T (&Di)[N], const T (&tv)[N], con
 
 template <typename T, int N, bool FAST, typename Tau, typename Out>
 RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&load_tau, Out &&out) {
-    T cs[N], sn[N], C[N], tv[N];
+    T cs[N], sn[N], C[N], tv[N], H[N][N], Di[N];
     if constexpr (RB_FDH_TAU_AT == 0) load_tau(tv);
     fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C);
     if constexpr (RB_FDH_TAU_AT == 1) load_tau(tv);
-    T H[N][N], Di[N];
-    if constexpr (RB_FDH_TAU_AT >= 2) {
-        fdh_factor<T, N>(mdl, cs, sn, H, Di);
-        load_tau(tv);
-    } else {
-        fdh_factor<T, N>(mdl, cs, sn, H, Di);
-    }
+    fdh_factor<T, N>(mdl, cs, sn, H, Di);
+    if constexpr (RB_FDH_TAU_AT >= 2) load_tau(tv);
     fdh_solve<T, N>(H, Di, tv, C, static_cast<Out &&>(out));
 }
 

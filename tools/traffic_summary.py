@@ -50,7 +50,9 @@ def main():
             for k, xs in sorted(v.items()):
                 w.writerow([k, sum(xs) / len(xs), min(xs), max(xs), len(xs)])
                 per[k] = sum(xs) / len(xs)
-    n, B = 7, int(workload.rsplit("_b", 1)[1])
+    model = workload.split("_")[1] if workload.startswith(("rnea_", "fd_")) else "fr3"
+    n = 7 if model == "fr3" else int(model[5:]) if model.startswith("chain") else 7
+    B = int(workload.rsplit("_b", 1)[1])
     es = 4 if "_f32_" in workload else 8
     alg = (8 if workload.startswith("rnea_fd") else 4) * n * es * B
     kind = workload.split("_")[0]
