@@ -152,9 +152,10 @@ int multibody_fd_batch_f64(const Multibody *mb, const double *q, const double *q
                            void *stream);
 /* Tiled layout (same computation): every array is [ceil(batch/256)][rows][256], element
  * (row j, configuration b) at ((b / 256) * rows + j) * 256 + b % 256, rows = n -- each
- * 256-configuration tile of all joints contiguous.  On MI355X this reaches 5.97 TB/s on
- * the RNEA pattern vs 4.68 TB/s for plain SoA rows (probe).  Allocate whole
- * tiles; lanes past `batch` in the last tile are neither read nor written. */
+ * 256-configuration tile of all joints contiguous.  Measured on MI355X (interleaved, one
+ * process): fp64 RNEA 3-4% faster than SoA rows, fp32 RNEA 5-8% slower, fp64 FD equal
+ *  -- use it when the data is produced tiled, not by converting.  Allocate
+ * whole tiles; lanes past `batch` in the last tile are neither read nor written. */
 int multibody_rnea_batch_tiled_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
                                    float *tau, int64_t batch, void *stream);
 int multibody_rnea_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
