@@ -171,7 +171,7 @@ int rb_from_tiled_f32(const float *src, float *dst, int64_t ld, int rows, int64_
 int rb_from_tiled_f64(const double *src, double *dst, int64_t ld, int rows, int64_t batch, void *stream);
 
 /* Fused rollout for MPC shooting: K steps of semi-implicit Euler on the forward dynamics
- * above (Articulated-Body form), qd += dt * qdd(q, qd, tau_k); q += dt * qd, the state
+ * above (the same algorithm the fd entry points use), qd += dt * qdd(q, qd, tau_k); q += dt * qd, the state
  * kept on chip between steps (LDS for fp32 chains up to 16 links, registers otherwise).  q and qd
  * ([n][ld]) are read and overwritten with the final state; tau_seq is [K][n][ld] (step k,
  * joint j, config b at (k*n + j)*ld + b); traj (same shape, may be NULL) receives q after

@@ -6,6 +6,7 @@
 // (multibody.rs:155-174) -- the reference has no forward-dynamics solve.
 #pragma once
 
+#include "fdh_body.hip.hpp"
 #include "tree_body.hip.hpp"
 
 namespace rbamd {
@@ -208,6 +209,23 @@ __device__ __forceinline__ void aba_lane_seq2(const T *mdl, const T *__restrict_
     if (two) aba_any<T, N, FAST, Topo>(mdl, qb, qdb, tb, [&](int j, T v) { st_row(qdd, j * ld, offB, v); });
 }
 
+// Forward dynamics inside the fused rollout: the mass-matrix form (fdh_body.hip.hpp) when
+// RB_ROLLOUT_FDH is set (jit.cpp: serial chains the fd_form policy gives it), else the ABA.
+// load_tau(tv) fills the step's torques: for the mass-matrix form after its bias sweep.
+#ifndef RB_ROLLOUT_FDH
+#define RB_ROLLOUT_FDH 0
+#endif
+template <typename T, int N, bool FAST, typename Topo, typename Tau, typename Out>
+RB_HD void rollout_fd(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&load_tau, Out &&out) {
+    if constexpr (RB_ROLLOUT_FDH != 0 && Topo::kSerial) {
+        fdh_eval<T, N, FAST>(mdl, qv, qdv, static_cast<Tau &&>(load_tau), static_cast<Out &&>(out));
+    } else {
+        T tv[N];
+        load_tau(tv);
+        aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, static_cast<Out &&>(out));
+    }
+}
+
 // Fused rollout (the MPC-shooting use of forward dynamics): K steps
 // of semi-implicit Euler, qd += dt * fd(q, qd, tau_k); q += dt * qd.  q, qd [n][ld] are
 // read once and overwritten with the final state; tau_seq is [K][n][ld]; traj
@@ -247,15 +265,18 @@ __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T 
         for (int k = 0; k < K; ++k) {
             int64_t ldk = ld;  // RB_ROLLOUT_NO_HOIST (jit.cpp): row offsets re-derived per step
             if constexpr (RB_ROLLOUT_NO_HOIST != 0) asm volatile("" : "+s"(ldk));
-            T qv[N], qdv[N], tv[N];
+            T qv[N], qdv[N];
 #pragma unroll
             for (int j = 0; j < N; ++j) {
                 qv[j] = sx[j * kRolloutBlock];
                 qdv[j] = sx[(N + j) * kRolloutBlock];
-                tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ldk, off);
             }
-            // aba_eval fences memory before its last pass, so these re-read LDS.
-            aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T a) {
+            auto load_tau = [&](T (&tv)[N]) {
+#pragma unroll
+                for (int j = 0; j < N; ++j) tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ldk, off);
+            };
+            // both forms fence memory before their last sweep, so these re-read LDS.
+            rollout_fd<T, N, FAST, Topo>(mdl, qv, qdv, load_tau, [&](int j, T a) {
                 const T qdn = fmadd(dt, a, sx[(N + j) * kRolloutBlock]);
                 const T qn = fmadd(dt, qdn, sx[j * kRolloutBlock]);
                 sx[(N + j) * kRolloutBlock] = qdn;
@@ -276,10 +297,12 @@ __device__ __forceinline__ void rollout_lane(const T *mdl, T *__restrict__ q, T 
             qdv[j] = ld_row(qd, j * ld, off);
         }
         for (int k = 0; k < K; ++k) {
-            T tv[N], a[N];
+            T a[N];
+            auto load_tau = [&](T (&tv)[N]) {
 #pragma unroll
-            for (int j = 0; j < N; ++j) tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
-            aba_any<T, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, T v) { a[j] = v; });
+                for (int j = 0; j < N; ++j) tv[j] = ld_row(tau_seq, ((int64_t)k * N + j) * ld, off);
+            };
+            rollout_fd<T, N, FAST, Topo>(mdl, qv, qdv, load_tau, [&](int j, T v) { a[j] = v; });
 #pragma unroll
             for (int j = 0; j < N; ++j) {
                 qdv[j] = fmadd(dt, a[j], qdv[j]);
@@ -327,14 +350,17 @@ __device__ __forceinline__ void rollout_lane2(const f2 *mdl, float *__restrict__
         // hold 2N 64-bit values in SGPRs, spilled to VGPRs, across every step
         int64_t ldk = ld;
         asm volatile("" : "+s"(ldk));
-        f2 qv[N], qdv[N], tv[N];
+        f2 qv[N], qdv[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) {
             qv[j] = sx[j * kRolloutBlock];
             qdv[j] = sx[(N + j) * kRolloutBlock];
-            tv[j] = ld_row2(tau_seq, ((int64_t)k * N + j) * ldk, offA, offB);
         }
-        aba_any<f2, N, FAST, Topo>(mdl, qv, qdv, tv, [&](int j, f2 a) {
+        auto load_tau = [&](f2 (&tv)[N]) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) tv[j] = ld_row2(tau_seq, ((int64_t)k * N + j) * ldk, offA, offB);
+        };
+        rollout_fd<f2, N, FAST, Topo>(mdl, qv, qdv, load_tau, [&](int j, f2 a) {
             const f2 qdn = fmadd(dt2, a, sx[(N + j) * kRolloutBlock]);
             const f2 qn = fmadd(dt2, qdn, sx[j * kRolloutBlock]);
             sx[(N + j) * kRolloutBlock] = qdn;

@@ -138,6 +138,10 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
     o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
     if (kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack)) o << "#define RB_ROLLOUT_NO_HOIST 1\n";
+    // the rollout's forward dynamics follows the fd_form policy (mass-matrix form for short
+    // serial chains) unless RB_VARIANT bit 8 (A/B) keeps the ABA
+    if (kind == JitKind::Rollout && jit_fd_form(m) == 2 && !(tuning().jit_variant & 256))
+        o << "#define RB_ROLLOUT_FDH 1\n";
     const bool tab = jit_f64_tab(f64);
     o << "#define RB_SINCOS_TAB " << (tab ? 1 : 0) << "\n";
     // Split joint rotation (artinertia.hip.hpp to_parent_split): pays only when every R_p is a

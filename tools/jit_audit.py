@@ -28,6 +28,8 @@ def main():
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffinite-math-only",
            "-fno-signed-zeros", "-I", CSRC, "--cuda-device-only", "-S", "-o", os.path.join(d, "k.s"),
            "-Rpass-analysis=kernel-resource-usage", path]
+    if kind == "rollout" and "RB_ROLLOUT_NO_HOIST 1" in src:  # as jit.cpp compiles it
+        cmd[1:1] = ["-mllvm", "-disable-machine-licm"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:
         print(r.stderr[-4000:])
