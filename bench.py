@@ -430,6 +430,9 @@ def side_workloads(mb7, a):
                                              for k in kernel.split("_"))}
         if graph:  # the same launches replayed from a HIP graph; rates over the launches replayed
             gl = r["graph_launches"]
+            # eager back-to-back launches from Python are host-bound when the graph replay of the
+            # same launches is faster: the graph line is then the device-bound rate
+            sec[name]["host_bound"] = bool(r["kernel_ms_avg"] > 1.05 * r["graph_kernel_ms_avg"])
             sec[name + "_graph"] = {"evals_per_s": B * gl / r["graph_wall"],
                                     "kernel_ms_avg": r["graph_kernel_ms_avg"], "batch": B, "layout": layout,
                                     "dtype": dt_name, "launches": gl,
