@@ -160,6 +160,31 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         }
     const int sr = tuning().split_rot;
     o << "#define RB_SPLIT_ROT " << ((sr > 0 || (sr < 0 && perm)) ? 1 : 0) << "\n";
+    // Newton-Euler link forces about the centre of mass (spatial.hip.hpp link_force) for the
+    // serial chains' RNEA sweeps: c = h / m and Ic = I_o - m (|c|^2 1 - c c^T) per link, in
+    // fp64 here.  jit_variant bit 9 (A/B) keeps the origin form.  Not for the fp64 RNEA: the
+    // memory-bound headline kernel gains nothing from fewer VALU and its sequential pair would
+    // need 131 instead of 125 VGPRs (3 waves/SIMD instead of 4).
+    if (m.serial_revolute() && !(kind == JitKind::Rnea && f64) && !(tuning().jit_variant & 512)) {
+        o << "#define RB_COM_FORM 1\n";
+        o << "static __device__ constexpr double rb_com[" << 9 * m.n << "] = {\n";
+        for (int i = 0; i < m.n; ++i) {
+            const double *L = &pk[(size_t)i * kLinkStride];
+            const double mass = L[kM];
+            double c[3] = {0, 0, 0};
+            if (mass > 0)
+                for (int k = 0; k < 3; ++k) c[k] = L[kH + k] / mass;
+            const double cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+            const double Ic[6] = {L[kIo + 0] - mass * (cc - c[0] * c[0]), L[kIo + 1] + mass * c[0] * c[1],
+                                  L[kIo + 2] + mass * c[0] * c[2],        L[kIo + 3] - mass * (cc - c[1] * c[1]),
+                                  L[kIo + 4] + mass * c[1] * c[2],        L[kIo + 5] - mass * (cc - c[2] * c[2])};
+            o << "  ";
+            for (int k = 0; k < 3; ++k) o << literal(c[k], true) << ", ";
+            for (int k = 0; k < 6; ++k) o << literal(Ic[k], true) << ", ";
+            o << "\n";
+        }
+        o << "};\n";
+    }
     o << (kind == JitKind::Rnea                               ? "#include \"rnea_body.hip.hpp\"\n"
           : fdh                                               ? "#include \"fdh_body.hip.hpp\"\n"
           : (kind == JitKind::Fd || kind == JitKind::Rollout) ? "#include \"aba_body.hip.hpp\"\n"

@@ -27,13 +27,7 @@ RB_HD void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn,
     st.v = v3(T(0), T(0), T(0));
     st.aw = v3(T(0), T(0), qdd0);
     st.av = v3(g * E.m[6], g * E.m[7], g * E.m[8]);  // E^T (0,0,g)
-    // I v with v = (w, 0):  n = I_o w,  f = -h x w
-    const V3<T> In = v3(L.Io.xz * qd0, L.Io.yz * qd0, L.Io.zz * qd0);
-    const V3<T> If = v3(-L.h.y * qd0, L.h.x * qd0, T(0));  // -h x (0,0,qd)
-    V3<T> An, Af;
-    inertia_mul(L, st.aw, st.av, An, Af);
-    ff = cross_add(Af, st.w, If);
-    fn = cross_add(An, st.w, In);
+    link_force(L, 0, st.w, st.v, st.aw, st.av, fn, ff);  // v = 0 folds away
 }
 
 // Link j >= 1: forward sweep step (multibody.rs:122-141).
@@ -56,11 +50,7 @@ RB_HD void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, 
     awn.y = fmadd(-wn.x, qdj, awn.y);
     st.w = wn; st.v = vn; st.aw = awn; st.av = avn;
     // f = I a + v x* (I v)   (multibody.rs:140)
-    V3<T> In, If, An, Af;
-    inertia_mul(L, st.w, st.v, In, If);
-    inertia_mul(L, st.aw, st.av, An, Af);
-    ff = cross_add(Af, st.w, If);
-    fn = cross_add(cross_add(An, st.w, In), st.v, If);
+    link_force(L, j, st.w, st.v, st.aw, st.av, fn, ff);
 }
 
 // Backward sweep step: f_{j-1} += X_j^-1 f_j  (multibody.rs:145-150).

@@ -251,6 +251,45 @@ RB_HD void inertia_mul(const Link<T> &L, const V3<T> &w, const V3<T> &v,
     f = cross_sub(v3(L.m * v.x, L.m * v.y, L.m * v.z), L.h, w);  // m v - h x w
 }
 
+// Link force f = I a + v x* (I v) (inertia.rs:107-117, spatial.rs:129-134) for a link moving
+// with (w, v) and accelerating with (aw, av), both spatial, in link coordinates.
+// Model-specialised kernels of serial chains (RB_COM_FORM, jit.cpp) evaluate it as the
+// Newton-Euler equations about the centre of mass c with the COM inertia Ic (per-link
+// constants rb_com[9j..] = c, Ic, computed on the host in fp64 from m, h, I_o):
+//   vc = v + w x c,  ac = a + aw x c,  f = m (ac + w x vc),  n = Ic aw + w x (Ic w) + c x f
+// -- the same quantity (f is m times the COM's classical acceleration, n Euler's equation
+// moved to the link origin) in 51 instead of 66 FMAs.
+#ifndef RB_COM_FORM
+#define RB_COM_FORM 0
+#endif
+#if RB_COM_FORM
+template <typename T>
+RB_HD T com_k(double x) { return T(x); }
+template <>
+RB_HD f2 com_k<f2>(double x) { return f2{(float)x, (float)x}; }
+template <typename T>
+RB_HD void link_force(const Link<T> &L, int j, const V3<T> &w, const V3<T> &v, const V3<T> &aw, const V3<T> &av,
+                      V3<T> &fn, V3<T> &ff) {
+    const double *k = rb_com + 9 * j;
+    const V3<T> c = v3(com_k<T>(k[0]), com_k<T>(k[1]), com_k<T>(k[2]));
+    const S3<T> Ic{com_k<T>(k[3]), com_k<T>(k[4]), com_k<T>(k[5]), com_k<T>(k[6]), com_k<T>(k[7]), com_k<T>(k[8])};
+    const V3<T> vc = cross_add(v, w, c);
+    const V3<T> g = cross_add(cross_add(av, aw, c), w, vc);
+    ff = v3(L.m * g.x, L.m * g.y, L.m * g.z);
+    fn = cross_add(cross_add(mul(Ic, aw), w, mul(Ic, w)), c, ff);
+}
+#else
+template <typename T>
+RB_HD void link_force(const Link<T> &L, int, const V3<T> &w, const V3<T> &v, const V3<T> &aw, const V3<T> &av,
+                      V3<T> &fn, V3<T> &ff) {
+    V3<T> In, If, An, Af;
+    inertia_mul(L, w, v, In, If);
+    inertia_mul(L, aw, av, An, Af);
+    ff = cross_add(Af, w, If);
+    fn = cross_add(cross_add(An, w, In), v, If);
+}
+#endif
+
 // SoA row access: uniform row base (SGPRs) + a 32-bit per-lane byte offset, so loads and
 // stores use the global_load/store saddr form with one shared offset VGPR instead of a
 // 64-bit address per access.  Callers keep b * sizeof(T) < 2^32 (per-launch batch cap).
