@@ -132,11 +132,7 @@ RB_HD void rnea_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
         AW[j] = aw;
         AV[j] = av;
         // f = I a + v x* (I v)   (multibody.rs:140)
-        V3<T> In, If, An, Af;
-        inertia_mul(L, w, v, In, If);
-        inertia_mul(L, aw, av, An, Af);
-        ff[j] = cross_add(Af, w, If);
-        fn[j] = cross_add(cross_add(An, w, In), v, If);
+        link_force(L, j, w, v, aw, av, fn[j], ff[j]);
     });
     reload_fence();
     cfor_rev<N>([&](auto jc) {  // tau_j = S_j^T f_j; f_parent += X_j^T f_j  (multibody.rs:143-150)
