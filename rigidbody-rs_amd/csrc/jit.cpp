@@ -163,11 +163,12 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // Newton-Euler link forces about the centre of mass (spatial.hip.hpp link_force) for the
     // RNEA sweeps of chains and trees (and so the mass-matrix FD's bias): c = h / m and
     // Ic = I_o - m (|c|^2 1 - c c^T) per link (massless virtual links: c = 0, Ic = I_o = 0), in
-    // fp64 here.  jit_variant bit 9 (A/B) keeps the origin form.  Not for the fp64 sequential-
-    // pair RNEA: the memory-bound headline kernel gains nothing from fewer VALU and would need
-    // 131 instead of 125 VGPRs (3 waves/SIMD instead of 4).
+    // fp64 here.  jit_variant bit 9 (A/B) keeps the origin form.  Not for the fp64 RNEA: the
+    // memory-bound headline kernel gains nothing from fewer VALU, its sequential pair would need
+    // 131 instead of 125 VGPRs (3 waves/SIMD instead of 4), and all its grid forms (pairs,
+    // single tail, one per lane below 2^19) must stay bit-identical to each other.
     const bool dyn = kind == JitKind::Rnea || kind == JitKind::Fd || kind == JitKind::Rollout;
-    if (dyn && !(kind == JitKind::Rnea && f64 && pack == 3) && !(tuning().jit_variant & 512)) {
+    if (dyn && !(kind == JitKind::Rnea && f64) && !(tuning().jit_variant & 512)) {
         o << "#define RB_COM_FORM 1\n";
         o << "static __device__ constexpr double rb_com[" << 9 * m.n << "] = {\n";
         for (int i = 0; i < m.n; ++i) {
