@@ -225,7 +225,8 @@ def barrier(world):
 
 def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1, sync_every=0):
     """launch(i, stream_ptr) issues step i.  Warmup, then exactly `steps` launches
-    bracketed by barrier + synchronize and one hipEvent pair on the launch stream (no
+    bracketed by barrier + synchronize on both sides (the clock stops at the closing
+    synchronize, before the closing barrier) and one hipEvent pair on the launch stream (no
     per-launch events inside the timed region: an event record between launches on one
     stream inflates a ~22 us step to ~32 us).  With streams > 1 consecutive steps rotate
     over that many streams; the event pair then spans all of them.
@@ -260,8 +261,10 @@ def time_launches(launch, steps, warmup, world, spinup_ms=0.0, streams=1, sync_e
         main.wait_event(end)
     e1.record(main)
     torch.cuda.synchronize()
-    barrier(world)
+    # the region ends at this rank's synchronize; the barrier after it only re-aligns the
+    # ranks (its collective latency is not step time), and max over ranks takes the slowest
     t1 = time.perf_counter()
+    barrier(world)
     return t1 - t0, e0.elapsed_time(e1) / steps
 
 
