@@ -190,6 +190,12 @@ int multibody_fwd_kin_batch_f64(const Multibody *mb, const double *q, double *po
                                 int64_t batch, int64_t ld, void *stream);
 int multibody_jac_batch_f64(const Multibody *mb, const double *q, double *J,
                             int64_t batch, int64_t ld, void *stream);
+/* The same in fp32 (the reference computes them in fp64, lib.rs:46-70; fp32 for callers that
+ * keep their batch in fp32). */
+int multibody_fwd_kin_batch_f32(const Multibody *mb, const float *q, float *pos,
+                                int64_t batch, int64_t ld, void *stream);
+int multibody_jac_batch_f32(const Multibody *mb, const float *q, float *J,
+                            int64_t batch, int64_t ld, void *stream);
 
 /* ---- batched host-pointer entry points (blocking) ------------------------------ */
 int multibody_rnea_batch_host_f64(const Multibody *mb, const double *q, const double *qd,

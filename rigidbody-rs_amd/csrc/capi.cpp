@@ -309,15 +309,17 @@ hipError_t launch_crba_any(const Multibody *mb, const T *mdl, const T *q, T *H, 
     return rbamd::launch_crba<T>(mb->model.n, mdl, q, H, B, ld, s);
 }
 
-// fwd_kin / jac (fp64): the precompiled kernels for serial revolute chains, hipRTC kernels
+// fwd_kin / jac: the precompiled kernels for serial revolute chains, hipRTC kernels
 // (tree_body.hip.hpp) for trees and prismatic joints.
-hipError_t launch_kin_any(const Multibody *mb, bool jac, const double *mdl, const double *q, double *out, uint32_t B,
-                          int64_t ld, hipStream_t s) {
+template <typename T>
+hipError_t launch_kin_any(const Multibody *mb, bool jac, const T *mdl, const T *q, T *out, uint32_t B, int64_t ld,
+                          hipStream_t s) {
     if (B == 0) return hipSuccess;
+    const bool fast = sizeof(T) == 4 && fast_trig();
     if (mb->model.serial_revolute())
-        return jac ? rbamd::launch_jac<double>(mb->model.n, mdl, q, out, B, ld, s)
-                   : rbamd::launch_fwd_kin<double>(mb->model.n, mdl, q, out, B, ld, s);
-    const rbamd::JitKernel *jk = jit_get(mb, jac ? rbamd::JitKind::Jac : rbamd::JitKind::FwdKin, true, false);
+        return jac ? rbamd::launch_jac<T>(mb->model.n, mdl, q, out, B, ld, s, fast)
+                   : rbamd::launch_fwd_kin<T>(mb->model.n, mdl, q, out, B, ld, s, fast);
+    const rbamd::JitKernel *jk = jit_get(mb, jac ? rbamd::JitKind::Jac : rbamd::JitKind::FwdKin, sizeof(T) == 8, fast);
     if (!jk) return no_generic(mb);
     void *args[] = {(void *)&q, (void *)&out, (void *)&B, (void *)&ld};
     return jit_launch(jk, B, args, s);
@@ -488,6 +490,20 @@ int crba_batch(const Multibody *mb, const T *q, T *H, int64_t batch, int64_t ld,
     });
 }
 
+template <typename T>
+int kin_batch(const Multibody *mb, bool jac, const T *q, T *out, int64_t batch, int64_t ld, void *stream) {
+    int rc = check_batch(mb, batch, ld);
+    if (rc) return rc;
+    if (batch == 0) return RB_OK;
+    if (!q || !out) return set_err(RB_ERR_NULL, "NULL array");
+    const T *mdl = nullptr;
+    if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
+        hipError_t e = launch_kin_any<T>(mb, jac, mdl, q + b0, out + b0, nb, ld, (hipStream_t)stream);
+        return e == hipSuccess ? RB_OK : hip_err(e, jac ? "jac launch" : "fwd_kin launch");
+    });
+}
+
 Multibody *new_from_text(const std::string &xml, unsigned flags = 0) {
     try {
         return make(rbamd::Model::from_urdf_text(xml, flags));
@@ -635,7 +651,7 @@ double *multibody_fwd_kin(const Multibody *mb, const double *q) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
         if (rc) return rc;
-        hipError_t e = launch_kin_any(mb, false, mdl, din, dout, 1, 1, s);
+        hipError_t e = launch_kin_any<double>(mb, false, mdl, din, dout, 1, 1, s);
         return e == hipSuccess ? RB_OK : hip_err(e, "fwd_kin launch");
     });
 }
@@ -652,7 +668,7 @@ double *multibody_jac(const Multibody *mb, const double *q) {
         const double *mdl = nullptr;
         int rc = device_consts<double>(mb, &mdl);
         if (rc) return rc;
-        hipError_t e = launch_kin_any(mb, true, mdl, din, dout, 1, 1, s);
+        hipError_t e = launch_kin_any<double>(mb, true, mdl, din, dout, 1, 1, s);
         return e == hipSuccess ? RB_OK : hip_err(e, "jac launch");
     });
 }
@@ -900,30 +916,19 @@ int multibody_crba_batch_f64(const Multibody *mb, const double *q, double *H, in
 
 int multibody_fwd_kin_batch_f64(const Multibody *mb, const double *q, double *pos, int64_t batch,
                                 int64_t ld, void *stream) {
-    int rc = check_batch(mb, batch, ld);
-    if (rc) return rc;
-    if (batch == 0) return RB_OK;
-    if (!q || !pos) return set_err(RB_ERR_NULL, "NULL array");
-    const double *mdl = nullptr;
-    if ((rc = device_consts<double>(mb, &mdl))) return rc;
-    return chunked<double>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = launch_kin_any(mb, false, mdl, q + b0, pos + b0, nb, ld, (hipStream_t)stream);
-        return e == hipSuccess ? RB_OK : hip_err(e, "fwd_kin launch");
-    });
+    return kin_batch<double>(mb, false, q, pos, batch, ld, stream);
 }
-
 int multibody_jac_batch_f64(const Multibody *mb, const double *q, double *J, int64_t batch, int64_t ld,
                             void *stream) {
-    int rc = check_batch(mb, batch, ld);
-    if (rc) return rc;
-    if (batch == 0) return RB_OK;
-    if (!q || !J) return set_err(RB_ERR_NULL, "NULL array");
-    const double *mdl = nullptr;
-    if ((rc = device_consts<double>(mb, &mdl))) return rc;
-    return chunked<double>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = launch_kin_any(mb, true, mdl, q + b0, J + b0, nb, ld, (hipStream_t)stream);
-        return e == hipSuccess ? RB_OK : hip_err(e, "jac launch");
-    });
+    return kin_batch<double>(mb, true, q, J, batch, ld, stream);
+}
+int multibody_fwd_kin_batch_f32(const Multibody *mb, const float *q, float *pos, int64_t batch, int64_t ld,
+                                void *stream) {
+    return kin_batch<float>(mb, false, q, pos, batch, ld, stream);
+}
+int multibody_jac_batch_f32(const Multibody *mb, const float *q, float *J, int64_t batch, int64_t ld,
+                            void *stream) {
+    return kin_batch<float>(mb, true, q, J, batch, ld, stream);
 }
 
 // ------------------------------------------------------------- batched (host)

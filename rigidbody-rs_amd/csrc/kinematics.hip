@@ -149,13 +149,16 @@ __global__ __launch_bounds__(kBlock) void fill_uniform_kernel(T *__restrict__ x,
 
 template <typename T>
 hipError_t launch_fwd_kin(int n, const T *mdl, const T *q, T *pos, uint32_t B, int64_t ld,
-                          hipStream_t s) {
+                          hipStream_t s, bool fast) {
     if (B == 0) return hipSuccess;
     const dim3 grid(dev::grid_for(B)), block(dev::kBlock);
     switch (n) {
 #define RB_CASE(N)                                                                              \
     case N:                                                                                     \
-        hipLaunchKernelGGL((dev::fwd_kin_kernel<T, N, false>), grid, block, 0, s, mdl, q, pos, B, ld); \
+        if (fast)                                                                               \
+            hipLaunchKernelGGL((dev::fwd_kin_kernel<T, N, true>), grid, block, 0, s, mdl, q, pos, B, ld); \
+        else                                                                                    \
+            hipLaunchKernelGGL((dev::fwd_kin_kernel<T, N, false>), grid, block, 0, s, mdl, q, pos, B, ld); \
         break;
         RB_FOR_EACH_DOF(RB_CASE)
 #undef RB_CASE
@@ -167,13 +170,16 @@ hipError_t launch_fwd_kin(int n, const T *mdl, const T *q, T *pos, uint32_t B, i
 
 template <typename T>
 hipError_t launch_jac(int n, const T *mdl, const T *q, T *J, uint32_t B, int64_t ld,
-                      hipStream_t s) {
+                      hipStream_t s, bool fast) {
     if (B == 0) return hipSuccess;
     const dim3 grid(dev::grid_for(B)), block(dev::kBlock);
     switch (n) {
 #define RB_CASE(N)                                                                              \
     case N:                                                                                     \
-        hipLaunchKernelGGL((dev::jac_kernel<T, N, false>), grid, block, 0, s, mdl, q, J, B, ld); \
+        if (fast)                                                                               \
+            hipLaunchKernelGGL((dev::jac_kernel<T, N, true>), grid, block, 0, s, mdl, q, J, B, ld); \
+        else                                                                                    \
+            hipLaunchKernelGGL((dev::jac_kernel<T, N, false>), grid, block, 0, s, mdl, q, J, B, ld); \
         break;
         RB_FOR_EACH_DOF(RB_CASE)
 #undef RB_CASE
@@ -212,8 +218,13 @@ template hipError_t launch_to_tiled<float>(const float *, int64_t, float *, int,
 template hipError_t launch_to_tiled<double>(const double *, int64_t, double *, int, uint32_t, hipStream_t);
 template hipError_t launch_from_tiled<float>(const float *, float *, int64_t, int, uint32_t, hipStream_t);
 template hipError_t launch_from_tiled<double>(const double *, double *, int64_t, int, uint32_t, hipStream_t);
-template hipError_t launch_fwd_kin<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t);
-template hipError_t launch_jac<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t);
+template hipError_t launch_fwd_kin<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t,
+                                           bool);
+template hipError_t launch_jac<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t,
+                                       bool);
+template hipError_t launch_fwd_kin<float>(int, const float *, const float *, float *, uint32_t, int64_t, hipStream_t,
+                                          bool);
+template hipError_t launch_jac<float>(int, const float *, const float *, float *, uint32_t, int64_t, hipStream_t, bool);
 template hipError_t launch_fill_uniform<float>(float *, int, uint32_t, int64_t, const double *, uint64_t, hipStream_t);
 template hipError_t launch_fill_uniform<double>(double *, int, uint32_t, int64_t, const double *, uint64_t, hipStream_t);
 

@@ -79,6 +79,8 @@ for _t in ("f32", "f64"):
     _sig(f"multibody_crba_batch_{_t}", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
     _sig(f"rb_fill_uniform_{_t}", ctypes.c_int, [_vp, ctypes.c_int, _i64, _i64, _dp, _dp, ctypes.c_uint64, _vp])
 _sig("multibody_fwd_kin_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
+_sig("multibody_fwd_kin_batch_f32", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
+_sig("multibody_jac_batch_f32", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_jac_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_rnea_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
 _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
@@ -215,11 +217,11 @@ def _same_ld(ts):
 
 
 def _kin_out(out, rows, q):
-    """Output of fwd_kin / jac batches: [rows, B] float64 with the input's leading dimension."""
+    """Output of fwd_kin / jac batches: [rows, B] of q's dtype with the input's leading dimension."""
     B = q.shape[1]
-    if not isinstance(out, torch.Tensor) or out.dtype != torch.float64 or tuple(out.shape) != (rows, B) or \
+    if not isinstance(out, torch.Tensor) or out.dtype != q.dtype or tuple(out.shape) != (rows, B) or \
             (B > 1 and (out.stride(1) != 1 or out.stride(0) != _ld(q))):
-        raise ValueError(f"out must be a float64 [{rows}, {B}] tensor with the input's leading dimension")
+        raise ValueError(f"out must be a {q.dtype} [{rows}, {B}] tensor with the input's leading dimension")
 
 
 class Multibody:
@@ -456,27 +458,31 @@ class Multibody:
         return out
 
     def fwd_kin_batch(self, q, out=None, stream=None):
-        q = _soa(q, self.n, "q", torch.float64)
+        q = _soa(q, self.n, "q")
+        if q.dtype not in (torch.float32, torch.float64):
+            raise TypeError(f"q has dtype {q.dtype}, expected float32 or float64")
         B = q.shape[1]
         if out is None:
             out = torch.empty((3, _ld(q)), dtype=q.dtype, device=q.device)[:, :B]
         _kin_out(out, 3, q)
         dev = _one_device((q, out))
         with torch.cuda.device(dev):
-            _check(_lib.multibody_fwd_kin_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q),
-                                                    _stream_ptr(stream, dev)), "fwd_kin_batch")
+            fn = _lib.multibody_fwd_kin_batch_f64 if q.dtype == torch.float64 else _lib.multibody_fwd_kin_batch_f32
+            _check(fn(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q), _stream_ptr(stream, dev)), "fwd_kin_batch")
         return out
 
     def jac_batch(self, q, out=None, stream=None):
-        q = _soa(q, self.n, "q", torch.float64)
+        q = _soa(q, self.n, "q")
+        if q.dtype not in (torch.float32, torch.float64):
+            raise TypeError(f"q has dtype {q.dtype}, expected float32 or float64")
         B = q.shape[1]
         if out is None:
             out = torch.empty((6 * self.n, _ld(q)), dtype=q.dtype, device=q.device)[:, :B]
         _kin_out(out, 6 * self.n, q)
         dev = _one_device((q, out))
         with torch.cuda.device(dev):
-            _check(_lib.multibody_jac_batch_f64(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q),
-                                                _stream_ptr(stream, dev)), "jac_batch")
+            fn = _lib.multibody_jac_batch_f64 if q.dtype == torch.float64 else _lib.multibody_jac_batch_f32
+            _check(fn(self._h, q.data_ptr(), out.data_ptr(), B, _ld(q), _stream_ptr(stream, dev)), "jac_batch")
         return out
 
     # -------------------------------------------------------- batched, host [n, B]

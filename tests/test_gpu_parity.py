@@ -158,6 +158,13 @@ def test_batched_f32_vs_golden(name, ffi, dev, fr3_text):
     H32 = mb.crba_batch(q).cpu().numpy()
     Href = om.crba_batch(q64)
     _close(H32, Href, 1e-4, "crba f32")
+    # fp32 forward kinematics and body Jacobian (columns sampled; oracle on the rounded q)
+    pos32 = mb.fwd_kin_batch(q).cpu().numpy()
+    J32 = mb.jac_batch(q).cpu().numpy()
+    assert pos32.dtype == np.float32 and J32.dtype == np.float32
+    for b in range(0, q64.shape[1], max(1, q64.shape[1] // 64)):
+        _close(pos32[:, b], om.fwd_kin(q64[:, b]), 2e-5 * n, f"fwd_kin f32 b={b}")
+        _close(J32[:, b], om.jac_raw(q64[:, b]), 2e-5 * n, f"jac f32 b={b}")
 
 
 # ------------------------------------------------------------ shapes and edges

@@ -90,6 +90,14 @@ def test_tree_batched_f64(case, dev):
     assert np.array_equal(tau_t, mb.rnea_batch(_t(q, dev), _t(qd, dev), _t(qdd, dev)).cpu().numpy())
     qdd_t = ffi.from_tiled(mb.fd_batch_tiled(tq, tqd, ttin, B), B).cpu().numpy()
     assert np.array_equal(qdd_t, qdd_gpu)
+    # fp32 forward kinematics / Jacobian through the same hipRTC tree kernels
+    q32 = _t(q, dev).float()
+    q64 = q32.double().cpu().numpy()
+    pos32 = mb.fwd_kin_batch(q32).cpu().numpy()
+    J32 = mb.jac_batch(q32).cpu().numpy()
+    for b in range(0, B, 37):
+        _close(pos32[:, b], om.fwd_kin(q64[:, b]), 2e-5 * n, f"{case} fwd_kin f32")
+        _close(J32[:, b], om.jac_raw(q64[:, b]), 2e-5 * n, f"{case} jac f32")
 
 
 @pytest.mark.parametrize("case", CASES)
