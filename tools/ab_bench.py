@@ -2,7 +2,7 @@
 per cdna_hip_programming.md §5.4 rule 24.  Times the batched kernels over rotated
 input sets (> Infinity Cache) with a hipEvent pair around `steps` launches.
 
-usage: python tools/ab_bench.py [--kernel rnea|fd|rollout] [--dtype f32|f64] [--dof 7]
+usage: python tools/ab_bench.py [--kernel rnea|fd|rollout] [--dtype f32|f64] [--dof 7] [--graph]
                                 [--variants 'rnea_stream=0' 'rnea_stream=1,grid_factor=2' ...]
 """
 import argparse
@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--variants", nargs="+", default=["rnea_stream=0", "rnea_stream=1"],
                     help="comma-separated rb_set_tuning key=value lists; the pseudo-key 'streams' "
                          "sets how many HIP streams the timed launches rotate over")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the launches from a HIP graph (device-bound rate at small batches, where "
+                         "eager launches from Python are host-bound)")
     a = ap.parse_args()
     dtype = bench.DT[a.dtype]
     es = 4 if a.dtype == "f32" else 8
@@ -69,7 +72,10 @@ def main():
                     nstreams = int(val)
                     continue
                 assert lib.rb_set_tuning(k.encode(), int(val)) == 0, ffi.last_error()
-            _, ms = bench.time_launches(launches[lay], a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
+            if a.graph:  # captured per variant and round: the tuning picks the kernel at capture
+                _, ms, _ = bench.time_graph(launches[lay], a.steps, spinup_ms=50.0 if r == 0 else 10.0)
+            else:
+                _, ms = bench.time_launches(launches[lay], a.steps, 5, 1, 50.0 if r == 0 else 0.0, nstreams)
             res[(v, lay)].append(ms)
     out = {}
     for (v, lay), ms in res.items():
