@@ -452,6 +452,9 @@ def side_workloads(mb7, a):
     one("fd_fr3_f64", mb7, "fd", "f64")
     one("fd_fr3_f32", mb7, "fd", "f32", streams=(1, 2))
     one("rnea_fd_fr3_f64_b131072", mb7, "rnea_fd", "f64", 1 << 17, graph=True)  # config 4, one GPU's 2^17 shard
+    # SURVEY §8(e) scaling caveat: an extra large-batch point (2^24 configurations per launch,
+    # 3.8 GB per input set) where the launch's ramp and tail are amortised
+    one("rnea_fr3_f64_b16777216", mb7, "rnea", "f64", 1 << 24)
     mb30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     mb30.upload()
     one("rnea_chain30_f32", mb30, "rnea", "f32")             # config 5
