@@ -334,6 +334,10 @@ def batch_launcher(mb, sets, kernel, dtype, layout="soa", B=None):
             if fn(*args, sp):
                 raise RuntimeError(ffi.last_error())
 
+    # `calls` holds raw device pointers: the closure owns the tensors, or a caller that drops
+    # its `sets` leaves the launches on freed (and, after torch.cuda.graph's empty_cache,
+    # unmapped) memory
+    launch.keep = sets
     return launch
 
 

@@ -94,7 +94,7 @@ struct Multibody {
         const rbamd::JitKernel *jk;
     };
     mutable std::deque<JitPub> jit_pub;
-    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][4][2] = {};
+    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][5][2] = {};
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
@@ -182,7 +182,7 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     const bool fst = fast && !f64;
     const unsigned gen = rbamd::tuning_generation();
     std::atomic<const Multibody::JitPub *> *slot = nullptr;
-    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 4) {
+    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 5) {
         slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][tail > 0 ? 1 : 0];
         if (const Multibody::JitPub *p = slot->load(std::memory_order_acquire))
             if (p->gen == gen) return p->jk;
@@ -236,6 +236,23 @@ hipError_t no_generic(const Multibody *mb) {
 // Smallest batch for which the auto policy takes the paired-lane kernel: one resident round
 // of it (2 blocks of 512 configurations per CU x 256 CUs) -- 2^18.
 constexpr uint32_t kPackMinBatch = 1u << 18;
+// fp32 mass-matrix forward dynamics: below 2^17 configurations the split packed waves (jit
+// pack 4, fdh_split_block2), from 2^17 the packed pair -- FR3, HIP graph: 65536 4.05 us vs
+// 4.30 one per lane, 32768 4.00 vs 4.08; 131072 pair 5.36, one per lane 5.59, split 5.83.
+constexpr uint32_t kSplitMaxBatch = 1u << 17;
+
+// The forward-dynamics kernel a launch of B configurations takes (auto policy when the
+// tuning `pack` is unset).
+const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, bool fast, uint32_t B) {
+    int pack = 0;
+    if (rbamd::tuning().pack < 0) {
+        if (!f64 && rbamd::jit_fd_form(mb->model) == 2)
+            pack = B < kSplitMaxBatch ? 4 : 0;
+        else  // paired lanes halve the grid: below kPackMinBatch one per lane fills more CUs
+            pack = B < kPackMinBatch ? 1 : 0;
+    }
+    return jit_get(mb, rbamd::JitKind::Fd, f64, fast, pack);
+}
 
 unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
     if (jk->pack == 3 && jk->seq_tail > 0) {  // pairs, then a one-per-lane tail (jit.cpp)
@@ -272,10 +289,7 @@ template <typename T>
 hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *tau, T *qdd,
                          uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    // Paired lanes (jit_pack) halve the grid: below kPackMinBatch the one-per-lane kernel
-    // fills more CUs and wins (FR3 fp32 65536: 4.7 vs 5.2 us; 2^20: 31.0 vs 29.2 us).
-    const int pack = (rbamd::tuning().pack < 0 && B < kPackMinBatch) ? 1 : 0;
-    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Fd, sizeof(T) == 8, fast_trig(), pack)) {
+    if (const rbamd::JitKernel *jk = jit_fd(mb, sizeof(T) == 8, fast_trig(), B)) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau, (void *)&qdd, (void *)&B, (void *)&lda, (void *)&bs};
         return jit_launch(jk, B, args, s);
@@ -763,8 +777,7 @@ int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t bat
     if (kind == 0) {
         jk = jit_rnea(mb, f64 != 0, fast_trig(), B, tiled != 0);
     } else if (kind == 1) {
-        const int pack = (rbamd::tuning().pack < 0 && B < kPackMinBatch) ? 1 : 0;
-        jk = jit_get(mb, rbamd::JitKind::Fd, f64 != 0, fast_trig(), pack);
+        jk = jit_fd(mb, f64 != 0, fast_trig(), B);
     } else {
         jk = jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 || kind >= 4 ? false : fast_trig());
     }

@@ -191,5 +191,76 @@ __device__ __forceinline__ void fdh_lane2(const f2 *mdl, const float *__restrict
         [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
 }
 
+// Small batches on packed lanes (jit pack 4, fp32; capi.cpp jit_fd takes it below 2^17
+// configurations).  There the one-per-lane grid is at most one wave per SIMD and the kernel
+// time is the load burst plus ONE wave's dependent instruction stream (~1120 VALU at 65536);
+// the packed pair halves the instructions per configuration but, at two configurations per
+// lane, leaves half the SIMDs without a wave.  Here each pair of packed waves splits the work
+// instead: the bias wave evaluates C = rnea(q, qd, 0) for 128 configurations (two per lane),
+// the mass wave -- on another SIMD of the CU -- H and its L D L^T factorisation and, after one
+// block barrier that hands it C through LDS, the solve: ~590 instructions per wave.  A
+// 256-thread block covers one 256-configuration tile with two such pairs (waves 0/2 and 1/3:
+// configurations [0,128) and [128,256)), so the grid keeps the one-per-lane kernel's wave
+// count.  Both waves load q and evaluate (sin, cos); handing them over through LDS instead
+// (one more barrier, q read once) measured slower: 4.38 vs 4.05 us at 65536 (HIP graph), the
+// mass wave then waits for the bias wave's q rows.  Lanes past B read the tile's last
+// configuration and store nothing; every wave reaches the barrier.
+template <int N, bool FAST>
+__device__ __forceinline__ void fdh_split_block2(const f2 *mdl, const float *__restrict__ q,
+                                                 const float *__restrict__ qd, const float *__restrict__ tau,
+                                                 float *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {
+    __shared__ f2 shC[2][N][64];
+    const uint32_t w = threadIdx.x >> 6, g = w & 1u, l = threadIdx.x & 63u;
+    const uint32_t first = blockIdx.x * 256u;  // < B: the grid is ceil(B / 256) blocks
+    const uint32_t cA = (g << 7) + l, cB = cA + 64u, last = B - 1u - first;
+    const bool liveA = cA <= last, liveB = cB <= last;
+    const uint32_t offA = (liveA ? cA : last) * 4u;
+    const uint32_t offB = liveB ? cB * 4u : offA;
+    const int64_t o = (int64_t)blockIdx.x * bs;
+    if (w < 2) {
+        f2 qv[N], qdv[N], cs[N], sn[N], C[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row2(q + o, j * ld, offA, offB);
+            __builtin_amdgcn_sched_barrier(0);
+            qdv[j] = ld_row2(qd + o, j * ld, offA, offB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        fdh_bias<f2, N, FAST>(mdl, qv, qdv, cs, sn, C);
+#pragma unroll
+        for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
+        __syncthreads();
+    } else {
+        f2 qv[N], tv[N], cs[N], sn[N], C[N], H[N][N], Di[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row2(q + o, j * ld, offA, offB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            tv[j] = ld_row2(tau + o, j * ld, offA, offB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);
+        fdh_factor<f2, N>(mdl, cs, sn, H, Di);
+        // Everything above feeds only the liveA-guarded stores: without these pins the compiler
+        // sinks the loads and the mass-matrix work past the barrier, and the mass wave would
+        // start only after the bias wave has finished (5.69 vs 4.50 us at 65536, measured).
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            asm volatile("" : "+v"(Di[j].x), "+v"(Di[j].y));
+            asm volatile("" : "+v"(tv[j].x), "+v"(tv[j].y));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
+        fdh_solve<f2, N>(H, Di, tv, C, [&](int j, f2 v) {
+            if (liveA) st_row2(qdd + o, j * ld, offA, offB, v);
+        });
+    }
+}
+
 }  // namespace dev
 }  // namespace rbamd

@@ -76,3 +76,27 @@ def test_cpu_share_reads_the_cgroup_quota(tmp_path):
     assert bench.cpu_share(str(v1))[0] == min(2, vis)
     (v1 / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
     assert bench.cpu_share(str(v1))[0] == vis
+
+
+def test_batch_launcher_owns_its_sets():
+    """The launch closures hold raw device pointers; they must keep the tensors those point
+    to alive, or a caller that drops its input sets times kernels on freed memory (which a
+    HIP-graph capture's empty_cache then unmaps).  CPU tensors stand in for the sets; no
+    launch is issued."""
+    import gc
+    import types
+    import weakref
+
+    import torch
+
+    import bench
+
+    sets = [([torch.zeros(7, 8, dtype=torch.float64) for _ in range(3)], [torch.zeros(7, 8, dtype=torch.float64)])]
+    ref = weakref.ref(sets[0][0][0])
+    launch = bench.batch_launcher(types.SimpleNamespace(handle=None), sets, "rnea", torch.float64, "soa")
+    del sets
+    gc.collect()
+    assert ref() is not None
+    del launch
+    gc.collect()
+    assert ref() is None

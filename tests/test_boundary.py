@@ -247,7 +247,8 @@ def test_set_tuning_experimental_keys_gated(ffi):
 def test_jit_kernel_forms_compile(ffi, fr3_text):
     """Every model-specialised kernel form the production knobs select builds for gfx950
     (hipRTC, no device) and its source carries the form: paired fp32 forward-dynamics lanes
-    (pack; default for chains up to 8 links) or one per lane, table-assisted fp64 sincos,
+    (pack; default for chains up to 8 links), one per lane, or the small-batch split of packed
+    waves (pack 4, fp32 mass-matrix form only), table-assisted fp64 sincos,
     split joint rotation for signed-permutation frames."""
     from rigidbody_amd import chains
 
@@ -267,11 +268,15 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "RB_SPLIT_ROT 1" in mb.jit_source(False, "fd")  # FR3 frames are signed permutations
     try:
         for form, pack, marker in ((1, 2, "aba_lane2"), (1, 1, "aba_lane<"), (1, 3, "aba_lane_seq2<"),
-                                   (2, 2, "fdh_lane2<"), (2, 1, "fdh_lane<")):
+                                   (2, 2, "fdh_lane2<"), (2, 1, "fdh_lane<"), (2, 4, "fdh_split_block2<"),
+                                   (1, 4, "aba_lane<")):
             ffi.set_tuning("fd_form", form)
             ffi.set_tuning("pack", pack)
             assert marker in mb.jit_source(False, "fd"), (form, pack)
             assert mb.jit_compile(f64=False, kind="fd") > 1000, (form, pack)
+        ffi.set_tuning("fd_form", 2)
+        ffi.set_tuning("pack", 4)
+        assert "fdh_lane<" in mb.jit_source(True, "fd")  # pack 4 has no fp64 form
         ffi.set_tuning("pack", 1)
         assert "rnea_lane<" in mb.jit_source(True, "rnea")
     finally:

@@ -72,6 +72,7 @@ def main():
                     nstreams = int(val)
                     continue
                 assert lib.rb_set_tuning(k.encode(), int(val)) == 0, ffi.last_error()
+            print(f"round {r} variant {v} {lay}", file=sys.stderr, flush=True)
             if a.graph:  # captured per variant and round: the tuning picks the kernel at capture
                 _, ms, _ = bench.time_graph(launches[lay], a.steps, spinup_ms=50.0 if r == 0 else 10.0)
             else:

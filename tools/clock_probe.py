@@ -40,6 +40,7 @@ CASES = [
     ("fd_fr3_f64", "fd", True, 7, 4, 1, -1),
     ("fd_fr3_f32", "fd", False, 7, 4, 2, -1),
     ("fd_fr3_f32_p1", "fd", False, 7, 8, 1, 1),
+    ("fd_fr3_f32_p4", "fd", False, 7, 8, 1, 4),  # small-batch split: waves 0/1 bias, 2/3 mass matrix
     ("rnea_fr3_f32", "rnea", False, 7, 8, 1, -1),
     ("rnea_chain30_f32", "rnea", False, 30, 2, 1, -1),
 ]
@@ -123,6 +124,8 @@ def run(seconds, B, only):
             sys.exit(f"{co} missing: python tools/clock_probe.py build")
         mb = _model(dof)
         mb.upload()
+        if pack == 4:  # the split form runs only when selected (tuning pack 4)
+            assert ffi.lib().rb_set_tuning(b"pack", 4) == 0, ffi.last_error()
         n = mb.n
         dt = torch.float64 if f64 else torch.float32
         g = torch.Generator(device=dev).manual_seed(7)
@@ -150,7 +153,7 @@ def run(seconds, B, only):
         e1.record()
         torch.cuda.synchronize()
         product_us = e0.elapsed_time(e1) / 2000 * 1e3
-        if kind == "fd" and (pack == 1) != (B < (1 << 18)):
+        if kind == "fd" and pack != 4 and (pack == 1) != (B < (1 << 18)):
             sys.exit(f"{name}: the product launch at batch {B} takes a different form (capi.cpp kPackMinBatch)")
 
         module, fn = ctypes.c_void_p(), ctypes.c_void_p()
@@ -198,6 +201,15 @@ def run(seconds, B, only):
                 "in_kernel_span_us": round(span * 1e6, 2),
                 "residency": round(float(life.sum() / (1024 * wps * span)), 3),
                 "waves": waves, "waves_per_simd_limit": wps}
+        if pack == 4:  # per role: wave w % 4 in {0, 1} bias torques, {2, 3} mass matrix + solve
+            role = np.arange(waves) % 4 >= 2
+            t0 = s[:, 2].min()
+            for nm, sel in (("bias", ~role), ("mass", role)):
+                line[nm] = {"wave_us_median": round(float(np.median(life[sel])) * 1e6, 2),
+                            "start_us_median": round(float(np.median(s[sel, 2] - t0)) / 100, 2),
+                            "end_us_median": round(float(np.median(s[sel, 3] - t0)) / 100, 2),
+                            "end_us_max": round(float(np.max(s[sel, 3] - t0)) / 100, 2)}
+            assert ffi.lib().rb_set_tuning(b"pack", -1) == 0
         print(json.dumps(line), flush=True)
 
 
