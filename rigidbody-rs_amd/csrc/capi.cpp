@@ -94,7 +94,7 @@ struct Multibody {
         const rbamd::JitKernel *jk;
     };
     mutable std::deque<JitPub> jit_pub;
-    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][5][2] = {};
+    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][6][2] = {};
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
@@ -182,7 +182,7 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     const bool fst = fast && !f64;
     const unsigned gen = rbamd::tuning_generation();
     std::atomic<const Multibody::JitPub *> *slot = nullptr;
-    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 5) {
+    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 6) {
         slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][tail > 0 ? 1 : 0];
         if (const Multibody::JitPub *p = slot->load(std::memory_order_acquire))
             if (p->gen == gen) return p->jk;
@@ -236,9 +236,13 @@ hipError_t no_generic(const Multibody *mb) {
 // Smallest batch for which the auto policy takes the paired-lane kernel: one resident round
 // of it (2 blocks of 512 configurations per CU x 256 CUs) -- 2^18.
 constexpr uint32_t kPackMinBatch = 1u << 18;
-// fp32 mass-matrix forward dynamics: below 2^17 configurations the split packed waves (jit
-// pack 4, fdh_split_block2), from 2^17 the packed pair -- FR3, HIP graph: 65536 4.05 us vs
-// 4.30 one per lane, 32768 4.00 vs 4.08; 131072 pair 5.36, one per lane 5.59, split 5.83.
+// fp32 mass-matrix forward dynamics at small batches: one wave per SIMD at most, so the launch
+// time follows each wave's instruction stream; the wave splits (fdh_body.hip.hpp) halve it.
+// Up to 2^15 configurations the one-per-lane split (pack 5: B/32 waves), below 2^17 the
+// packed split (pack 4: B/64 waves), from 2^17 the packed pair.  FR3, HIP graph:
+// 32768 3.42 us (pack 5) / 3.77 (4) / 4.08 (one per lane); 65536 4.03 (4) / 4.30 (5) / 4.28 (1);
+// 131072 5.30 (4) / 5.37 (pair) / 5.62 (5) (profiles/r03/split/).
+constexpr uint32_t kSplit1MaxBatch = 1u << 15;
 constexpr uint32_t kSplitMaxBatch = 1u << 17;
 
 // The forward-dynamics kernel a launch of B configurations takes (auto policy when the
@@ -247,7 +251,7 @@ const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, bool fast, uint32_
     int pack = 0;
     if (rbamd::tuning().pack < 0) {
         if (!f64 && rbamd::jit_fd_form(mb->model) == 2)
-            pack = B < kSplitMaxBatch ? 4 : 0;
+            pack = B <= kSplit1MaxBatch ? 5 : B < kSplitMaxBatch ? 4 : 0;
         else  // paired lanes halve the grid: below kPackMinBatch one per lane fills more CUs
             pack = B < kPackMinBatch ? 1 : 0;
     }
@@ -261,7 +265,9 @@ unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
         const unsigned P = (T - S) & ~1u;
         return P / 2u + (T - P);
     }
-    const unsigned per_block = 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
+    // pack 2 / 3: two configurations per lane; pack 5: the one-per-lane wave split, 128 per block
+    // (pack 4, the packed split, covers 256 per block like one per lane)
+    const unsigned per_block = jk->pack == 5 ? 128u : 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
     return (unsigned)(((uint64_t)B + per_block - 1) / per_block);
 }
 

@@ -191,7 +191,7 @@ __device__ __forceinline__ void fdh_lane2(const f2 *mdl, const float *__restrict
         [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
 }
 
-// Small batches on packed lanes (jit pack 4, fp32; capi.cpp jit_fd takes it below 2^17
+// Small batches on packed lanes (jit pack 4, fp32; capi.cpp jit_fd takes it from 2^15 to 2^17
 // configurations).  There the one-per-lane grid is at most one wave per SIMD and the kernel
 // time is the load burst plus ONE wave's dependent instruction stream (~1120 VALU at 65536);
 // the packed pair halves the instructions per configuration but, at two configurations per
@@ -258,6 +258,66 @@ __device__ __forceinline__ void fdh_split_block2(const f2 *mdl, const float *__r
         for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
         fdh_solve<f2, N>(H, Di, tv, C, [&](int j, f2 v) {
             if (liveA) st_row2(qdd + o, j * ld, offA, offB, v);
+        });
+    }
+}
+
+// The same split one configuration per lane (jit pack 5; capi.cpp jit_fd takes it up to 2^15
+// configurations, where it keeps one wave per SIMD that the packed split would leave idle): a
+// 256-thread block covers 128 configurations -- half a 256-configuration tile -- with two wave
+// pairs (waves 0/2 and 1/3: configurations [0,64) and [64,128) of that half).  FR3 fp32 32768:
+// 3.42 us vs 3.77 packed split, 4.08 one per lane (HIP graph).  fp64 measured slower at every
+// size: its sincos is ~150 instructions, repeated by both waves.
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void fdh_split_block1(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                                 const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
+                                                 int64_t ld, int64_t bs) {
+    __shared__ T shC[2][N][64];
+    const uint32_t w = threadIdx.x >> 6, g = w & 1u, l = threadIdx.x & 63u;
+    const uint32_t tile = blockIdx.x >> 1, first = blockIdx.x * 128u;  // < B (grid ceil(B / 128))
+    const uint32_t c = ((blockIdx.x & 1u) << 7) + (g << 6) + l;       // within the tile
+    const uint32_t last = B - 1u - tile * 256u;
+    const bool live = first + (g << 6) + l < B;
+    const uint32_t off = (live ? c : last) * (uint32_t)sizeof(T);
+    const int64_t o = (int64_t)tile * bs;
+    if (w < 2) {
+        T qv[N], qdv[N], cs[N], sn[N], C[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+            qdv[j] = ld_row(qd + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C);
+#pragma unroll
+        for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
+        __syncthreads();
+    } else {
+        T qv[N], tv[N], cs[N], sn[N], C[N], H[N][N], Di[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            tv[j] = ld_row(tau + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);
+        fdh_factor<T, N>(mdl, cs, sn, H, Di);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            asm volatile("" : "+v"(Di[j]));
+            asm volatile("" : "+v"(tv[j]));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
+        fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) {
+            if (live) st_row(qdd + o, j * ld, off, v);
         });
     }
 }

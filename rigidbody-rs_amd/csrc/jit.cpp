@@ -85,6 +85,7 @@ int jit_pack(JitKind kind, bool f64, int n) {
     if (kind != JitKind::Fd && kind != JitKind::Rnea) return 1;
     if (v == 3) return 3;
     if (v == 4) return (kind == JitKind::Fd && !f64) ? 4 : 1;  // split packed waves (fdh_split_block2)
+    if (v == 5) return (kind == JitKind::Fd && !f64) ? 5 : 1;  // split waves, one per lane (fdh_split_block1)
     if (v >= 0) return (v >= 2 && !f64 && kind == JitKind::Fd) ? 2 : 1;
     if (kind == JitKind::Rnea) return (f64 && n <= 8) ? 3 : 1;
     return (!f64 && n <= 8) ? 2 : 1;
@@ -114,8 +115,8 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
     const int pack = pack_req > 0 ? pack_req : jit_pack(kind, f64, m.n);
     // the mass-matrix forward dynamics has one- and two-per-lane forms only
     if (kind == JitKind::Fd && pack == 3 && jit_fd_form(m) == 2) return 1;
-    // 4 = the packed bias / mass-matrix wave split: fp32 mass-matrix forward dynamics only
-    if (pack == 4 && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2)) return 1;
+    // 4 / 5 = the bias / mass-matrix wave split, packed / one per lane: fp32 mass-matrix FD only
+    if ((pack == 4 || pack == 5) && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2)) return 1;
     return pack;
 }
 
@@ -289,7 +290,9 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
-        if (fdh && pack == 4) {
+        if (fdh && pack == 5) {
+            o << "  rbamd::dev::fdh_split_block1<T, N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
+        } else if (fdh && pack == 4) {
             o << "  rbamd::dev::fdh_split_block2<N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
         } else if (fdh && pack == 2) {
             o << pair_prologue;

@@ -268,7 +268,7 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "RB_SPLIT_ROT 1" in mb.jit_source(False, "fd")  # FR3 frames are signed permutations
     try:
         for form, pack, marker in ((1, 2, "aba_lane2"), (1, 1, "aba_lane<"), (1, 3, "aba_lane_seq2<"),
-                                   (2, 2, "fdh_lane2<"), (2, 1, "fdh_lane<"), (2, 4, "fdh_split_block2<"),
+                                   (2, 2, "fdh_lane2<"), (2, 1, "fdh_lane<"), (2, 4, "fdh_split_block2<"), (2, 5, "fdh_split_block1<"),
                                    (1, 4, "aba_lane<")):
             ffi.set_tuning("fd_form", form)
             ffi.set_tuning("pack", pack)

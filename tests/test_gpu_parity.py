@@ -678,9 +678,10 @@ def test_fd_forms_vs_oracle(dt, ffi, dev, fr3_text):
     1 = Articulated-Body Algorithm (aba_body.hip.hpp), 2 = the mass-matrix method
     (fdh_body.hip.hpp: rnea(q, qd, 0) bias, CRBA H, L D L^T solve -- the oracle's own
     definition, SURVEY §8(a) A10 over multibody.rs:111-174), fp32 with one and two
-    configurations per lane and the small-batch split of packed waves (pack 4: bias wave and
-    mass-matrix wave joined through LDS, fdh_split_block2), SoA and tiled, at B = 1, 200, 255,
-    65536 (config 3) and the ragged 65539, against the oracle's CRBA solve:
+    configurations per lane and the small-batch wave splits (bias wave and mass-matrix wave
+    joined through LDS: pack 4 packed, fdh_split_block2; pack 5 one per lane, fdh_split_block1),
+    SoA and tiled, at B = 1, 200, 255, 32768, 65536 (config 3) and the ragged 65539, against the
+    oracle's CRBA solve:
       fp64: |qdd - qdd_oracle| <= 1e-9 max(1, cond(H)/1e3) (1 + |qdd|), torque residual 1e-8;
       fp32: the backward-error bound K <= 16 and the element-wise 1e-3 torque residual.
     SoA and tiled outputs of one kernel form are bit-identical."""
@@ -691,14 +692,14 @@ def test_fd_forms_vs_oracle(dt, ffi, dev, fr3_text):
     lim = mb.limits()
     dtype = torch.float64 if dt == "f64" else torch.float32
     npd = "float64" if dt == "f64" else "float32"
-    packs = (1,) if dt == "f64" else (1, 2, 4)
+    packs = (1,) if dt == "f64" else (1, 2, 4, 5)
     outs = {}
     try:
         for form in (1, 2):
             ffi.set_tuning("fd_form", form)
             for pack in packs:
                 ffi.set_tuning("pack", pack)
-                for B in (1, 200, 255, 65536, 65539):
+                for B in (1, 200, 255, 32768, 65536, 65539):
                     x = [chains.host_uniform(7, B, *chains.input_ranges(lim, k), chains.SEED + 11 + i, dtype=npd)
                          for i, k in enumerate(("q", "qd", "tau"))]
                     xt = [_t(a, dev, dtype) for a in x]
