@@ -477,6 +477,16 @@ def side_workloads(mb7, a):
                                         "launches": nl,
                                         "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", dn == "f64"),
                                         "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)"}
+    # the MPC-sized rollout (65536 configurations, K = 16): the split of packed waves per step
+    # (rollout_split_block2), device-bound rate from a HIP graph
+    Bs = 65536
+    rl = rollout_launcher(mb7, Bs, torch.float32, K)
+    nl = budget_steps(rl, lo=200)
+    w, km, gl = time_graph(rl, nl)
+    sec["rollout_fr3_f32_K16_b65536_graph"] = {"steps_per_launch": K, "batch": Bs, "evals_per_s": Bs * K * gl / w,
+                                               "launches": gl, "kernel_ms_avg": km,
+                                               "launch": "HIP graph of 100 captured C-ABI launches, replayed",
+                                               "note": "evals = configurations x Euler steps"}
     return sec
 
 

@@ -172,7 +172,8 @@ int rb_from_tiled_f64(const double *src, double *dst, int64_t ld, int rows, int6
 
 /* Fused rollout for MPC shooting: K steps of semi-implicit Euler on the forward dynamics
  * above (the same algorithm the fd entry points use), qd += dt * qdd(q, qd, tau_k); q += dt * qd, the state
- * kept on chip between steps (LDS for fp32 chains up to 16 links, registers otherwise).  q and qd
+ * kept on chip between steps (LDS for fp32 chains up to 16 links, registers otherwise; below
+ * 2^17 fp32 configurations each step is split over a pair of waves sharing the state in LDS).  q and qd
  * ([n][ld]) are read and overwritten with the final state; tau_seq is [K][n][ld] (step k,
  * joint j, config b at (k*n + j)*ld + b); traj (same shape, may be NULL) receives q after
  * every step. */

@@ -375,5 +375,87 @@ __device__ __forceinline__ void rollout_lane2(const f2 *mdl, float *__restrict__
     }
 }
 
+// Split rollout for small batches (jit pack 4, fp32 mass-matrix form; capi.cpp takes it below
+// 2^17 configurations): each Euler step is one forward dynamics, split over a pair of packed
+// waves as fdh_split_block2 splits one launch -- the bias wave evaluates C(q, qd) for 128
+// configurations, the mass wave H, L D L^T, then (block barrier A) the solve and the Euler
+// update of the state, which lives in LDS for both; block barrier B hands the new state to the
+// bias wave's next step.  Lanes past B compute on the tile's last configuration and store
+// nothing; every wave reaches both barriers K times.
+template <int N, bool FAST>
+__device__ __forceinline__ void rollout_split_block2(const f2 *mdl, float *__restrict__ q, float *__restrict__ qd,
+                                                     const float *__restrict__ tau_seq, float dt, int K,
+                                                     float *__restrict__ traj, uint32_t B, int64_t ld) {
+    __shared__ f2 shX[2][2 * N][64];  // per wave pair: q rows then qd rows, one f2 per lane
+    __shared__ f2 shC[2][N][64];
+    const uint32_t w = threadIdx.x >> 6, g = w & 1u, l = threadIdx.x & 63u;
+    const uint32_t first = blockIdx.x * 256u;  // < B: the grid is ceil(B / 256) blocks
+    const uint32_t cA = (g << 7) + l, cB = cA + 64u, last = B - 1u - first;
+    const bool liveA = cA <= last, liveB = cB <= last;
+    const uint32_t offA = (first + (liveA ? cA : last)) * 4u;
+    const uint32_t offB = liveB ? (first + cB) * 4u : offA;
+    f2(&sx)[2 * N][64] = shX[g];
+    const f2 dt2 = f2{dt, dt};
+    if (w < 2) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            sx[j][l] = ld_row2(q, j * ld, offA, offB);
+            sx[N + j][l] = ld_row2(qd, j * ld, offA, offB);
+        }
+    }
+    __syncthreads();
+    for (int k = 0; k < K; ++k) {
+        int64_t ldk = ld;  // row offsets re-derived per step (as rollout_lane2)
+        asm volatile("" : "+s"(ldk));
+        if (w < 2) {
+            f2 qv[N], qdv[N], cs[N], sn[N], C[N];
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                qv[j] = sx[j][l];
+                qdv[j] = sx[N + j][l];
+            }
+            fdh_bias<f2, N, FAST>(mdl, qv, qdv, cs, sn, C);
+#pragma unroll
+            for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
+            __syncthreads();  // A
+            __syncthreads();  // B
+        } else {
+            f2 qv[N], tv[N], cs[N], sn[N], C[N], H[N][N], Di[N];
+#pragma unroll
+            for (int j = 0; j < N; ++j) tv[j] = ld_row2(tau_seq, ((int64_t)k * N + j) * ldk, offA, offB);
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                qv[j] = sx[j][l];
+                sin_cos<FAST>(qv[j], sn[j], cs[j]);
+            }
+            fdh_factor<f2, N>(mdl, cs, sn, H, Di);
+            // keep the loads and the factorisation above barrier A (fdh_split_block2)
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                asm volatile("" : "+v"(Di[j].x), "+v"(Di[j].y));
+                asm volatile("" : "+v"(tv[j].x), "+v"(tv[j].y));
+            }
+            __syncthreads();  // A
+#pragma unroll
+            for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
+            fdh_solve<f2, N>(H, Di, tv, C, [&](int j, f2 a) {
+                const f2 qdn = fmadd(dt2, a, sx[N + j][l]);
+                const f2 qn = fmadd(dt2, qdn, sx[j][l]);
+                sx[N + j][l] = qdn;
+                sx[j][l] = qn;
+                if (traj && liveA) st_row2(traj, ((int64_t)k * N + j) * ldk, offA, offB, qn);
+            });
+            __syncthreads();  // B
+        }
+    }
+    if (w >= 2 && liveA) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            st_row2(q, j * ld, offA, offB, sx[j][l]);
+            st_row2(qd, j * ld, offA, offB, sx[N + j][l]);
+        }
+    }
+}
+
 }  // namespace dev
 }  // namespace rbamd

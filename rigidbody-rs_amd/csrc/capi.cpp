@@ -308,7 +308,13 @@ template <typename T>
 hipError_t launch_rollout_any(const Multibody *mb, const T *mdl, T *q, T *qd, const T *tau_seq, T dt, int K, T *traj,
                               uint32_t B, int64_t ld, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Rollout, sizeof(T) == 8, fast_trig())) {
+    // fp32 mass-matrix rollouts up to 2^17 configurations: the split of packed waves per step
+    // (aba_body.hip.hpp rollout_split_block2), as jit_fd's small-batch forward dynamics.  FR3,
+    // K = 16, HIP graph: 16384 43.3 vs 62.7 us (pair), 65536 43.6 vs 63.5, 131072 58.9 vs 63.7;
+    // 262144 101.5 vs 93.2 (profiles/r03/rollout_split/)
+    const int pack = (rbamd::tuning().pack < 0 && sizeof(T) == 4 && B <= kSplitMaxBatch &&
+                      rbamd::jit_fd_form(mb->model) == 2 && !(rbamd::tuning().jit_variant & 256)) ? 4 : 0;
+    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Rollout, sizeof(T) == 8, fast_trig(), pack)) {
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau_seq, (void *)&dt, (void *)&K, (void *)&traj,
                         (void *)&B, (void *)&ld};
         return jit_launch(jk, B, args, s);

@@ -52,7 +52,7 @@ int jit_nt(JitKind kind) {
 // per step): the paired fp32 form, and fp64 chains up to 8 links -- 212 instead of 264 VGPRs,
 // 2 waves/SIMD instead of 1: FR3 2^20 x 16 steps 641 vs 1027 us (12 links: no change; 30
 // links, state in registers: 6.09 vs 5.81 ms, so not there).
-bool jit_rollout_no_hoist(bool f64, int n, int pack) { return pack == 2 || (f64 && n <= 8); }
+bool jit_rollout_no_hoist(bool f64, int n, int pack) { return pack == 2 || pack == 4 || (f64 && n <= 8); }
 
 bool jit_opaque(JitKind kind, bool f64, int n) {
     const int v = tuning().opaque_consts;
@@ -64,7 +64,7 @@ bool jit_opaque(JitKind kind, bool f64, int n) {
 int jit_waves(JitKind kind, bool f64, int n) {
     const int v = tuning().jit_waves;
     if (v >= 0) return v;
-    if (kind == JitKind::Rollout && !f64 && n <= 8) return jit_pack(kind, f64, n) == 2 ? 2 : 4;
+    if (kind == JitKind::Rollout && !f64 && n <= 8) return jit_pack(kind, f64, n) != 1 ? 2 : 4;
     return 0;
 }
 
@@ -81,7 +81,7 @@ int jit_pack(JitKind kind, bool f64, int n) {
     // 42.0-42.8 us steady where the one-per-lane kernel alternates between ~40.7 and ~48.8 us
     // phases, mean 44.3-44.6).
     const int v = tuning().pack;
-    if (kind == JitKind::Rollout) return ((v < 0 || v == 2) && !f64 && n <= 8) ? 2 : 1;
+    if (kind == JitKind::Rollout) return ((v < 0 || v == 2 || v == 4) && !f64 && n <= 8) ? (v == 4 ? 4 : 2) : 1;
     if (kind != JitKind::Fd && kind != JitKind::Rnea) return 1;
     if (v == 3) return 3;
     if (v == 4) return (kind == JitKind::Fd && !f64) ? 4 : 1;  // split packed waves (fdh_split_block2)
@@ -116,7 +116,10 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
     // the mass-matrix forward dynamics has one- and two-per-lane forms only
     if (kind == JitKind::Fd && pack == 3 && jit_fd_form(m) == 2) return 1;
     // 4 / 5 = the bias / mass-matrix wave split, packed / one per lane: fp32 mass-matrix FD only
-    if ((pack == 4 || pack == 5) && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2)) return 1;
+    if (pack == 4 && kind == JitKind::Rollout && !(!f64 && jit_fd_form(m) == 2 && !(tuning().jit_variant & 256)))
+        return (!f64 && m.n <= 8) ? 2 : 1;  // the split needs the mass-matrix form: the pair instead
+    if ((pack == 4 || pack == 5) && kind != JitKind::Rollout && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2))
+        return 1;
     return pack;
 }
 
@@ -316,6 +319,10 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
             o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
             o << "  rbamd::dev::aba_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
         }
+    } else if (kind == JitKind::Rollout && pack == 4) {
+        o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
+             "int K, T *__restrict__ traj, uint32_t B, int64_t ld) {\n";
+        o << "  rbamd::dev::rollout_split_block2<N, " << F << ">(kModel, q, qd, tau_seq, dt, K, traj, B, ld);\n}\n";
     } else if (kind == JitKind::Rollout && pack == 2) {
         o << head << "rb_jit_kernel(T *__restrict__ q, T *__restrict__ qd, const T *__restrict__ tau_seq, T dt, "
              "int K, T *__restrict__ traj, uint32_t B, int64_t ld) {\n";

@@ -433,9 +433,10 @@ def test_rollout_vs_oracle(name, ffi, dev, fr3_text):
 @pytest.mark.parametrize("B", [777, 4100])
 def test_paired_rollout_vs_single_and_oracle(B, ffi, dev, fr3_text):
     """The paired fp32 rollout (two configurations per lane, the default for chains up to 8
-    links; lane t of batch blocks 2k and 2k+1) on ragged batches whose second block is partial
-    or absent, against the one-per-lane form (pack=1) and the oracle's step-by-step Euler on
-    spot columns of both halves."""
+    links from 2^17 configurations; lane t of batch blocks 2k and 2k+1) and the split rollout
+    (pack 4, the default below 2^17: bias wave + mass-matrix wave per step, state in LDS) on
+    ragged batches whose second block is partial or absent, against the one-per-lane form
+    (pack=1) and the oracle's step-by-step Euler on spot columns of both halves."""
     mb = ffi.Multibody.from_urdf_string(fr3_text)
     om = _oracle(fr3_text)
     K, dt = 8, 1e-3
@@ -445,25 +446,32 @@ def test_paired_rollout_vs_single_and_oracle(B, ffi, dev, fr3_text):
     ts = rng.uniform(-20, 20, (K, 7, B))
     out = {}
     try:
-        for pack in (1, -1):
+        for pack in (1, 2, 4, -1):
             ffi.set_tuning("pack", pack)
             q, qd = _t(q0, dev, torch.float32), _t(qd0, dev, torch.float32)
             tr = mb.rollout_batch(q, qd, torch.as_tensor(ts, dtype=torch.float32, device=dev).contiguous(), dt,
                                   traj=True)
             out[pack] = (q.cpu().numpy(), qd.cpu().numpy(), tr.cpu().numpy())
+        ffi.set_tuning("pack", 2)
+        assert "rollout_lane2" in mb.jit_source(False, "rollout")
+        ffi.set_tuning("pack", 4)
+        assert "rollout_split_block2" in mb.jit_source(False, "rollout")
     finally:
         ffi.set_tuning("pack", -1)
-    assert "rollout_lane2" in mb.jit_source(False, "rollout")
-    for a, b, what in zip(out[1], out[-1], ("q", "qd", "traj")):
-        assert np.isfinite(b).all()
-        _close(b, a, 1e-5, f"paired vs single rollout {what} B={B}")
-    cols = np.array([0, 255, 256, min(511, B - 1), 512, B - 1])
+    for pack in (2, 4):  # the split is bit-identical to the policy at these sizes (both pack 4)
+        for a, b, what in zip(out[1], out[pack], ("q", "qd", "traj")):
+            assert np.isfinite(b).all()
+            _close(b, a, 1e-5, f"pack {pack} vs single rollout {what} B={B}")
+    for a, b in zip(out[4], out[-1]):
+        np.testing.assert_array_equal(a, b)
+    cols = np.array([0, 127, 128, 255, 256, min(511, B - 1), 512, B - 1])
     cols = cols[cols < B]
     f32 = lambda x: x.astype(np.float32).astype(float)  # noqa: E731
     qr, qdr, trr = om.rollout_batch(f32(q0[:, cols]), f32(qd0[:, cols]), f32(ts[:, :, cols]), dt, want_traj=True)
-    _close(out[-1][0][:, cols], qr, 1e-4, "paired rollout q vs oracle")
-    _close(out[-1][1][:, cols], qdr, 1e-3, "paired rollout qd vs oracle")
-    _close(out[-1][2][:, :, cols], trr, 1e-4, "paired rollout traj vs oracle")
+    for pack in (2, 4):
+        _close(out[pack][0][:, cols], qr, 1e-4, f"pack {pack} rollout q vs oracle")
+        _close(out[pack][1][:, cols], qdr, 1e-3, f"pack {pack} rollout qd vs oracle")
+        _close(out[pack][2][:, :, cols], trr, 1e-4, f"pack {pack} rollout traj vs oracle")
 
 
 # ------------------------------------------------------------ tiled layout
