@@ -258,6 +258,17 @@ const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, bool fast, uint32_
     return jit_get(mb, rbamd::JitKind::Fd, f64, fast, pack);
 }
 
+// The rollout kernel a launch of B configurations takes: fp32 mass-matrix rollouts up to 2^17
+// configurations split every step over a pair of packed waves (aba_body.hip.hpp
+// rollout_split_block2), as jit_fd's small-batch forward dynamics.  FR3, K = 16, HIP graph:
+// 16384 43.3 vs 62.7 us (pair), 65536 43.6 vs 63.5, 131072 58.9 vs 63.7; 262144 101.5 vs 93.2
+// (profiles/r03/rollout_split/).
+const rbamd::JitKernel *jit_rollout(const Multibody *mb, bool f64, bool fast, uint32_t B) {
+    const int pack = (rbamd::tuning().pack < 0 && !f64 && B <= kSplitMaxBatch &&
+                      rbamd::jit_fd_form(mb->model) == 2 && !(rbamd::tuning().jit_variant & 256)) ? 4 : 0;
+    return jit_get(mb, rbamd::JitKind::Rollout, f64, fast, pack);
+}
+
 unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
     if (jk->pack == 3 && jk->seq_tail > 0) {  // pairs, then a one-per-lane tail (jit.cpp)
         const unsigned T = (unsigned)(((uint64_t)B + 255u) / 256u);
@@ -308,13 +319,7 @@ template <typename T>
 hipError_t launch_rollout_any(const Multibody *mb, const T *mdl, T *q, T *qd, const T *tau_seq, T dt, int K, T *traj,
                               uint32_t B, int64_t ld, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    // fp32 mass-matrix rollouts up to 2^17 configurations: the split of packed waves per step
-    // (aba_body.hip.hpp rollout_split_block2), as jit_fd's small-batch forward dynamics.  FR3,
-    // K = 16, HIP graph: 16384 43.3 vs 62.7 us (pair), 65536 43.6 vs 63.5, 131072 58.9 vs 63.7;
-    // 262144 101.5 vs 93.2 (profiles/r03/rollout_split/)
-    const int pack = (rbamd::tuning().pack < 0 && sizeof(T) == 4 && B <= kSplitMaxBatch &&
-                      rbamd::jit_fd_form(mb->model) == 2 && !(rbamd::tuning().jit_variant & 256)) ? 4 : 0;
-    if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Rollout, sizeof(T) == 8, fast_trig(), pack)) {
+    if (const rbamd::JitKernel *jk = jit_rollout(mb, sizeof(T) == 8, fast_trig(), B)) {
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau_seq, (void *)&dt, (void *)&K, (void *)&traj,
                         (void *)&B, (void *)&ld};
         return jit_launch(jk, B, args, s);
@@ -790,6 +795,8 @@ int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t bat
         jk = jit_rnea(mb, f64 != 0, fast_trig(), B, tiled != 0);
     } else if (kind == 1) {
         jk = jit_fd(mb, f64 != 0, fast_trig(), B);
+    } else if (kind == 3) {
+        jk = jit_rollout(mb, f64 != 0, fast_trig(), B);
     } else {
         jk = jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 || kind >= 4 ? false : fast_trig());
     }
