@@ -395,6 +395,40 @@ def test_cpp_consumer_drop_in(tmp_path, dev):
     _close(lines["crba"], g["crba_raw"], 1e-9, "consumer crba")
 
 
+
+def test_small_batch_fd_forms_strided(ffi, dev, fr3_text):
+    """The small-batch forward-dynamics forms (policy: the one-per-lane wave split, pack 5, up to
+    2^15; the packed wave split, pack 4) and the paired / one-per-lane forms through [7, ld]
+    buffers with ld > B: padding columns untouched, every form within the fp32 backward-error
+    bound of the oracle's CRBA solve, the policy's launch bit-identical to
+    pack 5."""
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    om = _oracle(fr3_text)
+    ld = 512
+    for B in (1, 64, 129, 300):
+        rng = np.random.default_rng(B + 17)
+        full = [torch.as_tensor(rng.uniform(lo, hi, (7, ld)), dtype=torch.float32, device=dev)
+                for lo, hi in ((-2.5, 2.5), (-1.5, 1.5), (-20.0, 20.0))]
+        x = [f[:, :B].cpu().numpy().astype(np.float64) for f in full]
+        res = {}
+        try:
+            for pack in (-1, 1, 2, 4, 5):
+                ffi.set_tuning("pack", pack)
+                out_full = torch.full((7, ld), 123.0, dtype=torch.float32, device=dev)
+                mb.fd_batch(full[0][:, :B], full[1][:, :B], full[2][:, :B], out=out_full[:, :B])
+                o = out_full.cpu().numpy()
+                assert np.all(o[:, B:] == 123.0), (B, pack)
+                res[pack] = o[:, :B].astype(np.float64)
+        finally:
+            ffi.set_tuning("pack", -1)
+        Hraw = om.crba_batch(x[0])
+        for pack, qdd in res.items():
+            assert np.isfinite(qdd).all(), (B, pack)
+            r = om.rnea_batch(x[0], x[1], qdd) - x[2]
+            assert fp32_fd_backward_ratio(r, Hraw, qdd, x[2]).max() <= FD32_BACKWARD_K, (B, pack)
+        np.testing.assert_array_equal(res[-1], res[5])  # the policy takes pack 5 at these sizes
+
+
 # ------------------------------------------------------------ fused rollout
 @pytest.mark.parametrize("name", ["fr3_golden.npz", "chain12_golden.npz"])
 def test_rollout_vs_oracle(name, ffi, dev, fr3_text):
