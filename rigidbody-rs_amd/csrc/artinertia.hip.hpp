@@ -196,6 +196,85 @@ RB_HD RigidI<T> rigid_to_parent(const M3<T> &Rp, T c, T s, const M3<T> &E, const
     return o;
 }
 
+// The composite step of crba_core in one pass: X^T I X (inertia.rs:81-89) plus the parent
+// link's own body (inertia.rs:96-105), for model-specialised kernels whose R_p is a constant
+// signed permutation (RB_SPLIT_ROT) and whose constants fold (not RB_OPAQUE_CONSTS).  With
+// P(h) = 2 (p.h) 1 - (h p^T + p h^T) (linear in h) and b = m p + h_parent:
+//   h'  = R_p (Rz h + R_p^T b)
+//   Io' = R_p (Rz Io Rz^T + K') R_p^T + P(h'),   K' = R_p^T (m (|p|^2 1 - p p^T) + Io_parent - P(b)) R_p
+// so every constant is the innermost addend of an FMA chain instead of a separate add (the
+// parent's 9 values, the parallel-axis constants).  The Rz congruence uses half the double
+// angle, C = cos(2q)/2 = 1/2 - s^2 and S = sin(2q)/2 = c s, and the trace it keeps:
+//   xx' = (xx + yy)/2 + w,  yy' = (xx + yy)/2 - w,  w = (xx - yy) C - 2 xy S
+//   xy' = (xx - yy) S + 2 xy C,  xz' = c xz - s yz,  yz' = s xz + c yz,  zz' = zz.
+// FR3 fp64: 27 instead of 33-35 VALU per composite step (tools/fd_stages.py).
+template <typename T>
+RB_HD M3<T> transpose(const M3<T> &R) {
+    return M3<T>{{R.m[0], R.m[3], R.m[6], R.m[1], R.m[4], R.m[7], R.m[2], R.m[5], R.m[8]}};
+}
+
+template <typename T>
+RB_HD S3<T> parallel_axis_p(const V3<T> &p, const V3<T> &h) {  // P(h) above
+    return S3<T>{T(2) * fmadd(p.y, h.y, p.z * h.z), -fmadd(h.x, p.y, p.x * h.y), -fmadd(h.x, p.z, p.x * h.z),
+                 T(2) * fmadd(p.x, h.x, p.z * h.z), -fmadd(h.y, p.z, p.y * h.z), T(2) * fmadd(p.x, h.x, p.y * h.y)};
+}
+
+// A folded model constant that enters as an FMA addend: pinned in SGPRs so the FMA reads it
+// there (VOP3 src2).  Left to the compiler, a 64-bit addend is copied into a VGPR pair with two
+// v_mov per use to feed the two-address v_fmac form (FR3 fp64: 55 extra VALU per launch).
+template <typename T>
+RB_HD T sconst(T v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (__builtin_constant_p(v)) asm volatile("" : "+s"(v));
+#endif
+    return v;
+}
+RB_HD f2 sconst(f2 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (__builtin_constant_p(v.x) && __builtin_constant_p(v.y) && v.x == v.y) {
+        float c = v.x;
+        asm volatile("" : "+s"(c));
+        return f2{c, c};
+    }
+#endif
+    return v;
+}
+
+template <typename T>
+RB_HD RigidI<T> rigid_to_parent_add(const M3<T> &Rp, T c, T s, const V3<T> &p, const RigidI<T> &I,
+                                    const Link<T> &Lp) {
+    const T m = I.m;
+    // constants (folded at compile time)
+    const V3<T> b = v3(fmadd(m, p.x, Lp.h.x), fmadd(m, p.y, Lp.h.y), fmadd(m, p.z, Lp.h.z));
+    const S3<T> Pb = parallel_axis_p(p, b);
+    const S3<T> K{fmadd(m, fmadd(p.y, p.y, p.z * p.z), Lp.Io.xx) - Pb.xx, fmadd(-m, p.x * p.y, Lp.Io.xy) - Pb.xy,
+                  fmadd(-m, p.x * p.z, Lp.Io.xz) - Pb.xz, fmadd(m, fmadd(p.x, p.x, p.z * p.z), Lp.Io.yy) - Pb.yy,
+                  fmadd(-m, p.y * p.z, Lp.Io.yz) - Pb.yz, fmadd(m, fmadd(p.x, p.x, p.y * p.y), Lp.Io.zz) - Pb.zz};
+    const M3<T> Rt = transpose(Rp);
+    const S3<T> Kf = rot_sym(Rt, K);
+    const V3<T> bf = mul(Rt, b);
+    const S3<T> Kr{sconst(Kf.xx), sconst(Kf.xy), sconst(Kf.xz), sconst(Kf.yy), sconst(Kf.yz), sconst(Kf.zz)};
+    const V3<T> br = v3(sconst(bf.x), sconst(bf.y), sconst(bf.z));
+    // per configuration
+    const S3<T> &S = I.Io;
+    const T sum = S.xx + S.yy, dif = S.xx - S.yy, xy2 = S.xy + S.xy;
+    const T C = fmadd(-s, s, T(0.5)), S2 = c * s;
+    const T w = fmadd(dif, C, -(xy2 * S2));
+    const S3<T> R{fmadd(T(0.5), sum, Kr.xx) + w, fmadd(dif, S2, fmadd(xy2, C, Kr.xy)),
+                  fmadd(c, S.xz, fmadd(-s, S.yz, Kr.xz)), fmadd(T(0.5), sum, Kr.yy) - w,
+                  fmadd(s, S.xz, fmadd(c, S.yz, Kr.yz)), S.zz + Kr.zz};
+    const V3<T> hr = v3(fmadd(c, I.h.x, fmadd(-s, I.h.y, br.x)), fmadd(s, I.h.x, fmadd(c, I.h.y, br.y)), I.h.z + br.z);
+    RigidI<T> o;
+    o.m = m + Lp.m;
+    o.h = mul(Rp, hr);
+    const S3<T> Io1 = rot_sym(Rp, R);
+    const V3<T> &h = o.h;
+    o.Io = S3<T>{fmadd(T(2) * p.y, h.y, fmadd(T(2) * p.z, h.z, Io1.xx)), fmadd(-p.y, h.x, fmadd(-p.x, h.y, Io1.xy)),
+                 fmadd(-p.z, h.x, fmadd(-p.x, h.z, Io1.xz)), fmadd(T(2) * p.x, h.x, fmadd(T(2) * p.z, h.z, Io1.yy)),
+                 fmadd(-p.z, h.y, fmadd(-p.y, h.z, Io1.yz)), fmadd(T(2) * p.x, h.x, fmadd(T(2) * p.y, h.y, Io1.zz))};
+    return o;
+}
+
 template <typename T>
 RB_HD void add_rigid(RigidI<T> &I, const Link<T> &L) {
     I.m += L.m;

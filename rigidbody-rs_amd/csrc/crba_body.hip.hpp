@@ -33,10 +33,16 @@ RB_HD void crba_core(const T *mdl, const T (&cs)[N], const T (&sn)[N], Out &&out
             out(j + N * i, Fn.z);
         }
         if (i > 0) {
+            RB_STAGE("crba_composite");
             const Link<T> L = load_link(mdl, i);
-            const M3<T> E = joint_rotation(L.Rp, cs[i], sn[i]);
-            Ic = rigid_to_parent(L.Rp, cs[i], sn[i], E, L.p, Ic);
-            add_rigid(Ic, load_link(mdl, i - 1));
+            if constexpr (RB_SPLIT_ROT != 0 && RB_OPAQUE_CONSTS == 0) {
+                Ic = rigid_to_parent_add(L.Rp, cs[i], sn[i], L.p, Ic, load_link(mdl, i - 1));
+            } else {
+                const M3<T> E = joint_rotation(L.Rp, cs[i], sn[i]);
+                Ic = rigid_to_parent(L.Rp, cs[i], sn[i], E, L.p, Ic);
+                add_rigid(Ic, load_link(mdl, i - 1));
+            }
+            RB_STAGE("crba_columns");
         }
     }
 }

@@ -36,43 +36,77 @@ namespace dev {
 
 // 1. bias torques C = rnea(q, qd, 0) (multibody.rs:111-153 with ddq = 0); also the joint
 // (cos, sin) the later stages reuse.
+// Model-specialised kernels whose R_p are signed permutations (RB_SPLIT_ROT) with centre-of-mass
+// link forces run the backward sweep (multibody.rs:143-150) in a fused form: the forward sweep
+// leaves each link's force as g = f / m (link_force_g), and each step computes the parent's
+// transmitted force as F_{j-1} = m_{j-1} g_{j-1} + E_j F_j and its moment as
+// n_{j-1} + E_j n_j + p_j x (E_j F_j) -- the link force's scaling and both accumulations become
+// FMAs with the child's terms as addends (E = R_p Rz(q) has two (cos, sin) rows and one +-e_z row
+// when R_p is a signed permutation).  FR3 fp64: 5 fewer VALU per link (tools/fd_stages.py).
 template <typename T, int N, bool FAST>
 RB_HD void fdh_bias(const T *mdl, const T (&qv)[N], const T (&qdv)[N], T (&cs)[N], T (&sn)[N], T (&C)[N]) {
-    V3<T> fn[N], ff[N];
+#if RB_COM_FORM
+    constexpr bool kG = RB_SPLIT_ROT != 0;
+#else
+    constexpr bool kG = false;
+#endif
+    V3<T> fn[N], ff[N];  // ff: the link force, or g = f / m (kG)
     RneaState<T> st;
-    rnea_fwd0<T, FAST>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0]);
+    rnea_fwd0<T, FAST, kG>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0]);
 #pragma unroll
-    for (int j = 1; j < N; ++j) rnea_fwd<T, FAST>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j]);
+    for (int j = 1; j < N; ++j) rnea_fwd<T, FAST, kG>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j]);
     reload_fence();
+    RB_STAGE("bias_bwd");
+    if constexpr (kG) {
+        const T ml = load_link(mdl, N - 1).m;
+        V3<T> F = v3(ml * ff[N - 1].x, ml * ff[N - 1].y, ml * ff[N - 1].z);
+        V3<T> n = fn[N - 1];
 #pragma unroll
-    for (int j = N - 1; j >= 1; --j) {
-        C[j] = fn[j].z;
-        rnea_bwd(mdl, j, cs[j], sn[j], ff[j], fn[j], ff[j - 1], fn[j - 1]);
+        for (int j = N - 1; j >= 1; --j) {
+            C[j] = n.z;
+            const Link<T> L = load_link(mdl, j);
+            const M3<T> E = joint_rotation(L.Rp, cs[j], sn[j]);
+            const V3<T> fl = mul(E, F);
+            const T mp = load_link(mdl, j - 1).m;
+            F = v3(fmadd(mp, ff[j - 1].x, fl.x), fmadd(mp, ff[j - 1].y, fl.y), fmadd(mp, ff[j - 1].z, fl.z));
+            n = cross_add(mul_add(fn[j - 1], E, n), L.p, fl);
+        }
+        C[0] = n.z;
+    } else {
+#pragma unroll
+        for (int j = N - 1; j >= 1; --j) {
+            C[j] = fn[j].z;
+            rnea_bwd(mdl, j, cs[j], sn[j], ff[j], fn[j], ff[j - 1], fn[j - 1]);
+        }
+        C[0] = fn[0].z;
     }
-    C[0] = fn[0].z;
 }
 
 // 3. H = L D L^T in place, root first: L[i][j] (i > j) overwrites H[j][i]; Di = 1 / D.
+// Row j's entries are kept unscaled, U[j][i] = L[i][j] D[j], until row i scales them: the
+// row starts by turning its column of U into L (L[j][k] = U[k][j] / D[k]), then
+//   D[j] = H[j][j] - sum_k L[j][k] U[k][j],   U[j][i] = H[j][i] - sum_k L[j][k] U[k][i]  (i > j)
+// -- one multiply per strictly-upper entry (n(n-1)/2) where scaling at the end of the row and
+// rebuilding L D at the next needs two.
 template <typename T, int N>
 RB_HD void fdh_ldl(T (&H)[N][N], T (&Di)[N]) {
-    T D[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        T w[N];  // w[k] = L[j][k] D[k]
         T d = H[j][j];
 #pragma unroll
         for (int k = 0; k < j; ++k) {
-            w[k] = H[k][j] * D[k];
-            d = fmadd(-H[k][j], w[k], d);
+            const T u = H[k][j];
+            const T l = u * Di[k];
+            d = fmadd(-l, u, d);
+            H[k][j] = l;
         }
-        D[j] = d;
         Di[j] = recip(d);
 #pragma unroll
         for (int i = j + 1; i < N; ++i) {
             T s = H[j][i];
 #pragma unroll
-            for (int k = 0; k < j; ++k) s = fmadd(-H[k][i], w[k], s);
-            H[j][i] = s * Di[j];
+            for (int k = 0; k < j; ++k) s = fmadd(-H[k][j], H[k][i], s);
+            H[j][i] = s;
         }
     }
 }
@@ -82,10 +116,12 @@ RB_HD void fdh_ldl(T (&H)[N][N], T (&Di)[N]) {
 template <typename T, int N>
 RB_HD void fdh_factor(const T *mdl, const T (&cs)[N], const T (&sn)[N], T (&H)[N][N], T (&Di)[N]) {
     reload_fence();
+    RB_STAGE("crba");
     crba_core<T, N>(mdl, cs, sn, [&](int e, T v) {
         const int j = e % N, i = e / N;
         if (j <= i) H[j][i] = v;
     });
+    RB_STAGE("ldl");
     fdh_ldl<T, N>(H, Di);
 }
 
@@ -114,10 +150,12 @@ template <typename T, int N, bool FAST, typename Tau, typename Out>
 RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&load_tau, Out &&out) {
     T cs[N], sn[N], C[N], tv[N], H[N][N], Di[N];
     if constexpr (RB_FDH_TAU_AT == 0) load_tau(tv);
+    RB_STAGE("bias_fwd");
     fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C);
     if constexpr (RB_FDH_TAU_AT == 1) load_tau(tv);
     fdh_factor<T, N>(mdl, cs, sn, H, Di);
     if constexpr (RB_FDH_TAU_AT >= 2) load_tau(tv);
+    RB_STAGE("solve");
     fdh_solve<T, N>(H, Di, tv, C, static_cast<Out &&>(out));
 }
 

@@ -151,6 +151,20 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << "#define RB_ROLLOUT_FDH 1\n";
     const bool tab = jit_f64_tab(f64);
     o << "#define RB_SINCOS_TAB " << (tab ? 1 : 0) << "\n";
+    if (tab) {  // (cos, sin)(k pi/128), k < 256, for sincos_tab (spatial.hip.hpp): long double, quadrants exact
+        const long double pi = 3.141592653589793238462643383279502884L;
+        o << "static __device__ constexpr double rb_sctab_src[512] = {\n";
+        for (int k = 0; k < 256; ++k) {
+            double c = (double)std::cos((long double)k * pi / 128.0L), s = (double)std::sin((long double)k * pi / 128.0L);
+            if (k % 64 == 0) {
+                const int q = k / 64;
+                c = q == 0 ? 1.0 : q == 2 ? -1.0 : 0.0;
+                s = q == 1 ? 1.0 : q == 3 ? -1.0 : 0.0;
+            }
+            o << "  " << literal(c, true) << ", " << literal(s, true) << ",\n";
+        }
+        o << "};\n";
+    }
     // Split joint rotation (artinertia.hip.hpp to_parent_split): pays only when every R_p is a
     // signed permutation (its congruence then folds away); a dense constant R_p (general-axis
     // frames, trees) makes it costlier than the folded E S E^T.

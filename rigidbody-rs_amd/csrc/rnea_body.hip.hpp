@@ -16,7 +16,8 @@ struct RneaState {
 };
 
 // Link 0: v_{-1} = 0, a_{-1} = (0, (0,0,+g)) -- multibody.rs:116-120
-template <typename T, bool FAST>
+// GF (centre-of-mass form only): ff receives g = f / m (spatial.hip.hpp link_force_g).
+template <typename T, bool FAST, bool GF = false>
 RB_HD void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn, T &cs,
                                           V3<T> &fn, V3<T> &ff) {
     const Link<T> L = load_link(mdl, 0);
@@ -27,11 +28,17 @@ RB_HD void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn,
     st.v = v3(T(0), T(0), T(0));
     st.aw = v3(T(0), T(0), qdd0);
     st.av = v3(g * E.m[6], g * E.m[7], g * E.m[8]);  // E^T (0,0,g)
+#if RB_COM_FORM
+    if constexpr (GF) {
+        link_force_g(L, 0, st.w, st.v, st.aw, st.av, fn, ff);
+        return;
+    }
+#endif
     link_force(L, 0, st.w, st.v, st.aw, st.av, fn, ff);  // v = 0 folds away
 }
 
 // Link j >= 1: forward sweep step (multibody.rs:122-141).
-template <typename T, bool FAST>
+template <typename T, bool FAST, bool GF = false>
 RB_HD void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, T &sn, T &cs,
                                          V3<T> &fn, V3<T> &ff) {
     const Link<T> L = load_link(mdl, j);
@@ -50,6 +57,12 @@ RB_HD void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, 
     awn.y = fmadd(-wn.x, qdj, awn.y);
     st.w = wn; st.v = vn; st.aw = awn; st.av = avn;
     // f = I a + v x* (I v)   (multibody.rs:140)
+#if RB_COM_FORM
+    if constexpr (GF) {
+        link_force_g(L, j, st.w, st.v, st.aw, st.av, fn, ff);
+        return;
+    }
+#endif
     link_force(L, j, st.w, st.v, st.aw, st.av, fn, ff);
 }
 

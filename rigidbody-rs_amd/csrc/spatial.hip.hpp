@@ -278,6 +278,19 @@ RB_HD void link_force(const Link<T> &L, int j, const V3<T> &w, const V3<T> &v, c
     ff = v3(L.m * g.x, L.m * g.y, L.m * g.z);
     fn = cross_add(cross_add(mul(Ic, aw), w, mul(Ic, w)), c, ff);
 }
+// The same wrench with the force left unscaled: g = f / m is returned and n uses c x f = h x g
+// (h = m c).  The forward dynamics' bias sweep (fdh_body.hip.hpp) multiplies by m in its backward
+// sweep, where the product takes the child's transmitted force as its FMA addend.
+template <typename T>
+RB_HD void link_force_g(const Link<T> &L, int j, const V3<T> &w, const V3<T> &v, const V3<T> &aw, const V3<T> &av,
+                        V3<T> &fn, V3<T> &g) {
+    const double *k = rb_com + 9 * j;
+    const V3<T> c = v3(com_k<T>(k[0]), com_k<T>(k[1]), com_k<T>(k[2]));
+    const S3<T> Ic{com_k<T>(k[3]), com_k<T>(k[4]), com_k<T>(k[5]), com_k<T>(k[6]), com_k<T>(k[7]), com_k<T>(k[8])};
+    const V3<T> vc = cross_add(v, w, c);
+    g = cross_add(cross_add(av, aw, c), w, vc);
+    fn = cross_add(cross_add(mul(Ic, aw), w, mul(Ic, w)), L.h, g);
+}
 #else
 template <typename T>
 RB_HD void link_force(const Link<T> &L, int, const V3<T> &w, const V3<T> &v, const V3<T> &aw, const V3<T> &av,
@@ -346,6 +359,25 @@ __device__ __forceinline__ void st_row(T *__restrict__ base, int64_t row, uint32
 // sweep instead of being kept live in VGPRs across the whole chain.
 RB_HD void reload_fence() { asm volatile("" ::: "memory"); }
 
+// Stage markers for the per-stage instruction audit (tools/fd_stages.py): an assembler comment
+// fenced by scheduling barriers, so the ISA splits where one stage ends.  Off in the product.
+#ifndef RB_STAGE_MARKS
+#define RB_STAGE_MARKS 0
+#endif
+#if RB_STAGE_MARKS
+#define RB_STAGE(name)                                       \
+    do {                                                     \
+        __builtin_amdgcn_sched_barrier(0);                   \
+        asm volatile("; rb_stage " name ::: "memory");       \
+        __builtin_amdgcn_sched_barrier(0);                   \
+    } while (0)
+#else
+#define RB_STAGE(name) \
+    do {               \
+    } while (0)
+#endif
+
+
 // ---------------------------------------------------------------------------- sincos
 // Joint angles need sin/cos once per link.  The ROCm device-library sincos carries a
 // Payne-Hanek branch for huge arguments that inflates every unrolled kernel's register
@@ -406,11 +438,16 @@ RB_HD void sin_cos(float x, float &s, float &c) {
     }
 }
 // Table-assisted fp64 sincos for the model-specialised fp64 kernels (RB_SINCOS_TAB, set by
-// jit.cpp): x = k pi/32 + r with |r| <= pi/64, (cos, sin)(k pi/32) from a 64-entry LDS table
-// the block fills once (sctab_init, wave 0 only), then degree-9/8 Taylor polynomials on r
-// (truncation < 1e-19) and one angle-addition step: ~22 VALU instructions per angle instead
-// of ~45 for sincos_cw's degree-13/14 minimax after a pi/2 reduction.  Entries come from
-// sincos_cw (<= 1 ulp), the result is within a few ulp of sin/cos(x).
+// jit.cpp): x = k pi/128 + r with |r| <= pi/256, (cos, sin)(k pi/128) from a 256-entry LDS table
+// the block copies once (sctab_init; the entries rb_sctab_src[2k], [2k+1] are computed on the host
+// in long double, quadrant points exact, and compiled into the hipRTC source), then a degree-5
+// minimax sine (leading term r exact, relative error <= 2.7e-17 on |r| <= 1.002 pi/256) and a
+// degree-6 Taylor cosine (truncation 1.3e-20), and one angle-addition step.  k comes from the
+// 1.5 * 2^52 shifter: fma(x, 128/pi, 1.5 * 2^52) rounds x 128/pi to the nearest integer and
+// leaves it, two's complement, in the low word -- the table index without a conversion.
+// 18 VALU instructions per angle (the previous pi/32 table: 23, plus ~65 on the block's first
+// wave to fill it); max error 2.8 ulp over |x| <= 100 (host emulation, 2e7 samples; the pi/32
+// table: 2.7).
 #ifndef RB_SINCOS_TAB
 #define RB_SINCOS_TAB 0
 #endif
@@ -418,34 +455,29 @@ RB_HD void sin_cos(float x, float &s, float &c) {
 struct alignas(16) SinCosEntry {
     double c, s;
 };
-__shared__ SinCosEntry rb_sctab[64];
+__shared__ SinCosEntry rb_sctab[256];
 
-// Every wave of the block must call this before any sin_cos(double) (it ends in a barrier).
+// Every wave of the block must call this before any sin_cos(double) (it ends in a barrier);
+// blocks are 256 threads, one entry each.
 __device__ __forceinline__ void sctab_init() {
-    if (threadIdx.x < 64) {
-        // pi/32 = (pi/2 split of sincos_cw) / 16, exact power-of-two scaling
-        const double a = __builtin_fma((double)threadIdx.x, 9.81747704246810386e-02,
-                                       (double)threadIdx.x * 3.82702124733547877e-18);
-        double s, c;
-        sincos_cw(a, s, c);
-        rb_sctab[threadIdx.x] = SinCosEntry{c, s};
-    }
+    const uint32_t t = threadIdx.x;
+    rb_sctab[t] = SinCosEntry{rb_sctab_src[2 * t], rb_sctab_src[2 * t + 1]};
     __syncthreads();
 }
 
 __device__ __forceinline__ void sincos_tab(double x, double &s, double &c) {
-    const double k = __builtin_rint(x * 1.01859163578813017e+01);  // 32/pi
-    double r = __builtin_fma(-k, 9.81747704246810386e-02, x);      // pi/32 hi (pi/2 hi / 16)
-    r = __builtin_fma(-k, 3.82702124733547877e-18, r);              // pi/32 mid
-    r = __builtin_fma(-k, -9.35865565536981143e-35, r);             // pi/32 lo
-    const SinCosEntry e = rb_sctab[(int)k & 63];
+    const double shifter = 6755399441055744.0;                      // 1.5 * 2^52
+    const double t = __builtin_fma(x, 4.074366543152521e+01, shifter);  // 128/pi
+    const double k = t - shifter;
+    const uint32_t ki = (uint32_t)__builtin_bit_cast(unsigned long long, t) & 255u;
+    double r = __builtin_fma(-k, 2.454369260617026e-02, x);         // pi/128 hi
+    r = __builtin_fma(-k, 9.567553118338697e-19, r);                 // pi/128 mid
+    r = __builtin_fma(-k, -2.3396639138424529e-35, r);               // pi/128 lo
+    const SinCosEntry e = rb_sctab[ki];
     const double z = r * r;
-    const double sr = __builtin_fma(r * z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
-                          2.75573192239858907e-06, -1.98412698412698413e-04), 8.33333333333333322e-03),
-                          -1.66666666666666657e-01), r);
-    const double cr = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, __builtin_fma(z,
-                          2.48015873015873016e-05, -1.38888888888888894e-03), 4.16666666666666644e-02),
-                          -0.5), 1.0);
+    const double sr = __builtin_fma(r * z, __builtin_fma(z, 8.333291563954032e-03, -1.666666666647126e-01), r);
+    const double cr = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, -1.3888888888888889e-03,
+                          4.1666666666666664e-02), -0.5), 1.0);
     s = __builtin_fma(e.s, cr, e.c * sr);
     c = __builtin_fma(e.c, cr, -(e.s * sr));
 }
