@@ -377,8 +377,15 @@ def budget_steps(launch, target_ms=SIDE_TARGET_MS, lo=SIDE_MIN_LAUNCHES, hi=SIDE
     return int(min(hi, max(lo, np.ceil(target_ms / max(ms, 1e-4)))))
 
 
+def per_rank(r, world, dev):
+    """[{rank, wall_s, kernel_ms_avg, steps}] of every rank, in rank order (per-GPU
+    device time beside the max-over-ranks line)."""
+    rows = rdist.gather_over_ranks([r["wall"], r["kernel_ms_avg"], r["steps"]], world, dev)
+    return [{"rank": k, "wall_s": w, "kernel_ms_avg": km, "steps": int(st)} for k, (w, km, st) in enumerate(rows)]
+
+
 def measure(mb, kernel, dt_name, B, layout, steps, warmup, world, rotate_gib, seed, spinup_ms=300.0, streams=1,
-            sync_every=0, graph=False, extra_streams=()):
+            sync_every=0, graph=False, extra_streams=(), dev=None):
     """Time `steps` launches of `kernel` over batches of B resident configurations (steps=None:
     a budget of ~SIDE_TARGET_MS of launches, budget_steps).  Returns a dict (wall,
     kernel_ms_avg, bytes, sets, steps) plus the graph-replay figures if asked."""
@@ -388,7 +395,9 @@ def measure(mb, kernel, dt_name, B, layout, steps, warmup, world, rotate_gib, se
     sets = make_sets(mb, B, ds, kernel, ns, seed, layout=layout)
     launch = batch_launcher(mb, sets, kernel, ds, layout, B)
     if steps is None:
-        steps = budget_steps(launch)
+        # every rank times the same launch count (the largest budget), so max-over-ranks compares
+        # equal work
+        steps = int(rdist.max_over_ranks([budget_steps(launch)], world, dev)[0]) if world > 1 else budget_steps(launch)
     wall, km = time_launches(launch, steps, warmup, world, spinup_ms, streams, sync_every)
     r = {"wall": wall, "kernel_ms_avg": km, "bytes": set_bytes(mb.n, B, es, kernel), "sets": ns, "steps": steps}
     if graph:
@@ -615,17 +624,22 @@ def main(a):
     B = hi - lo  # this rank's configurations per step
     global_batch = a.batch if strong else a.batch * world
     seed = chains.SEED if strong else rdist.rank_seed(chains.SEED, rank)
-    if a.stub:
+    def stub_measure(B_, steps):
         # plumbing rehearsal: same ranks, collectives and reporting, no device work
         t0 = time.perf_counter()
         barrier(world)
-        wall = time.perf_counter() - t0 + 1e-9
-        r = {"wall": wall, "kernel_ms_avg": wall / a.steps * 1e3, "bytes": set_bytes(n, B, esize, a.kernel), "sets": 0}
+        wall_ = time.perf_counter() - t0 + 1e-9
+        return {"wall": wall_, "kernel_ms_avg": wall_ / steps * 1e3, "bytes": set_bytes(n, B_, esize, a.kernel),
+                "sets": 0, "steps": steps}
+
+    if a.stub:
+        r = stub_measure(B, a.steps)
         kpath = "stub"
     else:
         r = measure(mb, a.kernel, a.dtype, B, a.layout, a.steps, a.warmup, world, a.rotate_gib, seed, a.spinup_ms,
                     a.streams, a.sync_every)
         kpath = "+".join(mb.kernel_path(k, a.dtype == "f64", B, a.layout == "tiled") for k in a.kernel.split("_"))
+    ranks = per_rank(r, world, dev)
     wall, kern_ms = rdist.max_over_ranks([r["wall"], r["kernel_ms_avg"]], world, dev)
     value = global_batch * a.steps / wall
     bytes_per_eval = set_bytes(n, 1, esize, a.kernel)
@@ -663,17 +677,31 @@ def main(a):
     }
     if traffic:
         line["roofline"]["traffic_source"] = f"profiles/traffic_{workload}.json (rocprofv3 PMC passes)"
+    if world > 1:
+        line["per_rank"] = ranks
     sec = {}
-    if world > 1 and not strong and not a.stub:
-        # the same global 2^20 batch sharded across the ranks, beside the weak line
+    if world > 1 and not strong:
+        # the same global 2^20 batch sharded across the ranks, beside the weak line.
+        # Its own launch budget (>= SIDE_MIN_LAUNCHES, ~SIDE_TARGET_MS, the same count on every
+        # rank): at N = 8 a 2^17 fp64 shard is ~7 us, so the driver's --steps 20 would time
+        # ~0.14 ms of work.
         slo, shi = rdist.shard(a.batch, rank, world)
-        rs = measure(mb, a.kernel, a.dtype, shi - slo, a.layout, a.steps, 5, world, a.rotate_gib, chains.SEED, 100.0)
+        if a.stub:
+            rs = stub_measure(shi - slo, SIDE_MIN_LAUNCHES)
+        else:
+            rs = measure(mb, a.kernel, a.dtype, shi - slo, a.layout, None, 5, world, a.rotate_gib, chains.SEED, 100.0,
+                         dev=dev)
         sw, sk = rdist.max_over_ranks([rs["wall"], rs["kernel_ms_avg"]], world, dev)
-        sec["strong_split"] = {"evals_per_s": a.batch * a.steps / sw, "global_batch": a.batch,
-                               "batch_per_gpu_max": -(-a.batch // world), "ms_per_step": sw / a.steps * 1e3,
-                               "kernel_ms_avg_max_rank": sk, "scaling": "strong"}
+        sec["strong_split"] = {"evals_per_s": a.batch * rs["steps"] / sw, "global_batch": a.batch,
+                               "batch_per_gpu_max": -(-a.batch // world), "launches": rs["steps"],
+                               "ms_per_step": sw / rs["steps"] * 1e3, "kernel_ms_avg_max_rank": sk,
+                               "per_rank": per_rank(rs, world, dev), "scaling": "strong",
+                               "timing": "own launch budget (bench.budget_steps, max over ranks), not --steps"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.stub:
         line["cpu_baseline"] = cpu_baseline(n, a.kernel, a.cpu_seconds)
+    elif world > 1:
+        line["cpu_baseline_note"] = ("not measured at world > 1: the CPU baseline runs on rank 0 of the 1-GPU "
+                                     "run only (bench.py --gpus 1), so the ranks' host cores stay idle here")
     if rank == 0 and not a.no_secondary and world == 1 and n == 7 and not a.stub:
         r2 = measure(mb, a.kernel, a.dtype, a.batch, a.layout, None, 5, 1, a.rotate_gib, seed, 50.0, 2)
         sec[f"{a.kernel}_{a.dtype}_{a.layout}_2streams"] = {

@@ -191,6 +191,53 @@ class Model:
         return H
 
 
+# ---- op counts of the reference formulation (oracle/flops.cpp) ---------------
+_flops = None
+
+
+def flops_lib():
+    """The op-counting build of oracle.c: same symbols, same binary layout (FlopD = one double)."""
+    global _flops
+    if _flops is None:
+        path = os.path.join(_HERE, "liboracle_flops.so")
+        if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(os.path.join(_HERE, "oracle.c")):
+            subprocess.run(["make", "-s", "-C", _HERE, "liboracle_flops.so"], check=True)
+        L = ctypes.CDLL(path)
+        L.oracle_rnea.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp]
+        L.oracle_crba.argtypes = [ctypes.c_void_p, _dp, _dp]
+        L.oracle_fd.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp]
+        L.oracle_fd.restype = ctypes.c_int
+        L.oracle_flops_get.argtypes = [ctypes.POINTER(ctypes.c_long)]
+        _flops = L
+    return _flops
+
+
+def op_counts(model: "Model", kind: str, q, qd=None, x=None) -> dict:
+    """Operations the reference's formulation executes for ONE evaluation (oracle.c under the
+    counting type): kind 'rnea' (x = qdd), 'crba', 'fd' (x = tau; the CRBA + RNEA(q, qd, 0) +
+    Cholesky definition).  flops = add + mul + div (+ sqrt); trig separate."""
+    L = flops_lib()
+    n = model.n
+    q = _c(q)
+    qd = _c(np.zeros(n) if qd is None else qd)
+    x = _c(np.zeros(n) if x is None else x)
+    out = np.zeros(n * n)
+    L.oracle_flops_reset()
+    if kind == "rnea":
+        L.oracle_rnea(model.ptr, _p(q), _p(qd), _p(x), _p(out))
+    elif kind == "crba":
+        L.oracle_crba(model.ptr, _p(q), _p(out))
+    elif kind == "fd":
+        L.oracle_fd(model.ptr, _p(q), _p(qd), _p(x), _p(out))
+    else:
+        raise ValueError(kind)
+    c = (ctypes.c_long * 5)()
+    L.oracle_flops_get(c)
+    add, mul, div, sq, trig = (int(v) for v in c)
+    return {"add": add, "mul": mul, "div": div, "sqrt": sq, "trig": trig, "flops": add + mul + div + sq,
+            "result": out[:n * n if kind == "crba" else n].copy()}
+
+
 # ---- primitives for the restated reference unit tests -----------------------
 def quat_from_scaled_axis(v):
     out = np.zeros(4)

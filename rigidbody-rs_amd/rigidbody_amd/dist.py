@@ -56,6 +56,16 @@ def max_over_ranks(values, world: int, device):
     return t.tolist()
 
 
+def gather_over_ranks(values, world: int, device):
+    """Every rank's list of floats, in rank order (per-rank device / wall times)."""
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    if world == 1:
+        return [t.tolist()]
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
 def sum_over_ranks(values, world: int, device):
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
     if world > 1:

@@ -38,6 +38,18 @@ def test_gpus2_spawns_two_ranks(split):
         assert cfg["global_batch"] == 1 << 20 and cfg["batch_per_gpu"] == 1 << 19
     assert line["value"] > 0 and line["metric"].startswith("RNEA evals/sec")
     assert line["dtype"] == "f64"  # the reference's Real (lib.rs:15)
+    # per-GPU times beside the max over ranks; no CPU baseline at world > 1, said so
+    assert [r["rank"] for r in line["per_rank"]] == [0, 1]
+    assert all(r["steps"] == 5 and r["wall_s"] > 0 for r in line["per_rank"])
+    assert "cpu_baseline" not in line and "world > 1" in line["cpu_baseline_note"]
+    if split == "weak":
+        # the strong split beside the weak line times its own launch budget, not --steps
+        import bench
+
+        st = line["secondary"]["strong_split"]
+        assert st["launches"] >= bench.SIDE_MIN_LAUNCHES
+        assert len(st["per_rank"]) == 2 and all(r["steps"] == st["launches"] for r in st["per_rank"])
+        assert st["global_batch"] == 1 << 20 and st["batch_per_gpu_max"] == 1 << 19
 
 
 def test_single_rank_default():

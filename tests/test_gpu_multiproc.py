@@ -129,3 +129,28 @@ def test_bench_two_ranks_strong_rnea_fd():
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["global_batch"] == 1 << 18 and line["config"]["batch_per_gpu"] == 1 << 17
     assert line["value"] > 0 and line["config"]["kernel_path"] == "jit+jit"
+    assert [x["rank"] for x in line["per_rank"]] == [0, 1] and all(x["kernel_ms_avg"] > 0 for x in line["per_rank"])
+
+
+def test_bench_two_ranks_weak_with_strong_split():
+    """The driver's N > 1 line shape (weak headline, --steps 20): the strong split beside it
+    times its own launch budget (>= SIDE_MIN_LAUNCHES on every rank), and both carry per-rank
+    device / wall times."""
+    import bench
+
+    e = dict(os.environ, RB_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--batch", str(1 << 18),
+                        "--steps", "20", "--warmup", "5", "--no-secondary", "--no-cpu-baseline", "--spinup-ms", "50",
+                        "--rotate-gib", "0.5"], capture_output=True, text=True, timeout=300, env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["steps"] == 20
+    assert len(line["per_rank"]) == 2 and all(x["steps"] == 20 for x in line["per_rank"])
+    st = line["secondary"]["strong_split"]
+    assert st["launches"] >= bench.SIDE_MIN_LAUNCHES
+    assert [x["steps"] for x in st["per_rank"]] == [st["launches"]] * 2
+    assert st["evals_per_s"] > 0 and "cpu_baseline" not in line
