@@ -117,6 +117,12 @@ int multibody_upload(const Multibody *mb);
 int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled);
 int multibody_kernel_path(const Multibody *mb, int kind, int f64);
 int multibody_rnea_kernel_path(const Multibody *mb, int f64);
+/* The launch form of that kernel (same resolution, compiles it if needed): 0 = precompiled
+ * generic kernel, else the model-specialised kernel's configurations-per-lane form -- 1 one per
+ * lane, 2 two per lane on packed fp32, 3 two per lane one after the other (fp64 RNEA), 4 / 5
+ * the bias / mass-matrix wave split packed / one per lane (fp32 mass-matrix forward dynamics
+ * and rollouts at small batches).  Negative = -status on a bad argument. */
+int multibody_kernel_form_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled);
 /* Where the reference's single-configuration queries (rigidbody.h: rnea, crba, fwd_kin,
  * jac) run for this model: 0 = on the calling host thread (the GPU lane bodies compiled for
  * the host; serial revolute chains of a precompiled DOF on an FMA3/AVX2 CPU), 1 = one GPU

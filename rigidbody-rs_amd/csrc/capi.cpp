@@ -86,14 +86,17 @@ struct Multibody {
     mutable std::map<std::string, rbamd::JitKernel> jit;
     mutable std::map<std::string, int> jit_device;
     // per-launch fast path of jit_get: [device][kind][f64][fast trig][requested pack][tail] ->
-    // the kernel resolved under one tuning generation, published as ONE pointer to an
-    // immutable {gen, kernel} record (records live in jit_pub and never move or die before
-    // free), so a reader never pairs a generation with another generation's kernel
+    // the kernel resolved under one tuning generation, published as ONE pointer to a record
+    // {generation, kernel}.  There is one record per (slot, kernel) pair, so the records are
+    // bounded by slots x kernels however often the tuning changes: a record's kernel never
+    // changes, its generation is re-stamped only when ITS slot resolves to that kernel again,
+    // and records live in jit_pub (std::map nodes never move) until free.  A reader that sees
+    // the current generation in the record its slot points at has that slot's kernel.
     struct JitPub {
-        unsigned gen;
-        const rbamd::JitKernel *jk;
+        std::atomic<unsigned> gen{0};
+        const rbamd::JitKernel *jk = nullptr;
     };
-    mutable std::deque<JitPub> jit_pub;
+    mutable std::map<std::pair<const void *, const rbamd::JitKernel *>, JitPub> jit_pub;
     mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][6][2] = {};
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
@@ -180,32 +183,45 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
     const bool fst = fast && !f64;
-    const unsigned gen = rbamd::tuning_generation();
     std::atomic<const Multibody::JitPub *> *slot = nullptr;
     if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 6) {
         slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][tail > 0 ? 1 : 0];
         if (const Multibody::JitPub *p = slot->load(std::memory_order_acquire))
-            if (p->gen == gen) return p->jk;
+            if (p->gen.load(std::memory_order_acquire) == rbamd::tuning_generation()) return p->jk;
     }
-    if (pack <= 0) pack = rbamd::jit_model_pack(mb->model, kind, f64, 0);
-    if (!(kind == rbamd::JitKind::Rnea && pack == 3)) tail = 0;
-    const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
-                            (fst ? ":fast" : ":precise") + rbamd::jit_tag(kind, f64, mb->model.n) + ":q" +
-                            std::to_string(pack) + ":st" + std::to_string(tail);
+    const int pack_req = pack;
     std::lock_guard<std::mutex> lk(mb->mu);
-    auto it = mb->jit.find(key);
-    if (it == mb->jit.end()) {
-        it = mb->jit.emplace(key, rbamd::jit_build(mb->model, kind, f64, fst, pack, tail)).first;
-        mb->jit_device[key] = d;
+    // The tuning generation is a sequence count (tuning.cpp): odd while rb_set_tuning writes,
+    // bumped again after.  The key and the kernel source both read the tuning knobs, so they are
+    // resolved between two reads of one even generation; a write in between resolves again (a
+    // kernel built from a mix of two tunings is never stored under either key).
+    for (;;) {
+        const unsigned gen = rbamd::tuning_generation_stable();
+        int pk = pack_req > 0 ? pack_req : rbamd::jit_model_pack(mb->model, kind, f64, 0);
+        const int tl = (kind == rbamd::JitKind::Rnea && pk == 3) ? tail : 0;
+        const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
+                                (fst ? ":fast" : ":precise") + rbamd::jit_tag(kind, f64, mb->model.n) + ":q" +
+                                std::to_string(pk) + ":st" + std::to_string(tl);
+        auto it = mb->jit.find(key);
+        if (it == mb->jit.end()) {
+            rbamd::JitKernel built = rbamd::jit_build(mb->model, kind, f64, fst, pk, tl);
+            if (rbamd::tuning_generation() != gen) {  // the tuning moved under the build
+                if (built.module) (void)hipModuleUnload(built.module);
+                continue;
+            }
+            it = mb->jit.emplace(key, std::move(built)).first;
+            mb->jit_device[key] = d;
+        }
+        const rbamd::JitKernel *res = it->second.function ? &it->second : nullptr;
+        if (rbamd::tuning_generation() != gen) continue;
+        if (slot && res) {
+            Multibody::JitPub &rec = mb->jit_pub[{(const void *)slot, res}];
+            rec.jk = res;
+            rec.gen.store(gen, std::memory_order_release);
+            slot->store(&rec, std::memory_order_release);
+        }
+        return res;
     }
-    const rbamd::JitKernel *res = it->second.function ? &it->second : nullptr;
-    // publish only if the tuning did not change while this call resolved the kernel (the
-    // key above was built from the tuning state of generation `gen` or a later one)
-    if (slot && rbamd::tuning_generation() == gen) {
-        mb->jit_pub.push_back(Multibody::JitPub{gen, res});
-        slot->store(&mb->jit_pub.back(), std::memory_order_release);
-    }
-    return res;
 }
 
 // Smallest batch for which the auto policy takes the sequential-pair fp64 RNEA (jit_pack 3):
@@ -238,8 +254,9 @@ hipError_t no_generic(const Multibody *mb) {
 constexpr uint32_t kPackMinBatch = 1u << 18;
 // fp32 mass-matrix forward dynamics at small batches: one wave per SIMD at most, so the launch
 // time follows each wave's instruction stream; the wave splits (fdh_body.hip.hpp) halve it.
-// Up to 2^15 configurations the one-per-lane split (pack 5: B/32 waves), below 2^17 the
-// packed split (pack 4: B/64 waves), from 2^17 the packed pair.  FR3, HIP graph:
+// Up to 2^15 configurations the one-per-lane split (pack 5: B/32 waves), up to 2^17 the
+// packed split (pack 4: B/64 waves; the rollout's split takes the same bound), above it the
+// packed pair.  FR3, HIP graph:
 // 32768 3.42 us (pack 5) / 3.77 (4) / 4.08 (one per lane); 65536 4.03 (4) / 4.30 (5) / 4.28 (1);
 // 131072 5.30 (4) / 5.37 (pair) / 5.62 (5) (profiles/r03/split/).
 constexpr uint32_t kSplit1MaxBatch = 1u << 15;
@@ -251,7 +268,7 @@ const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, bool fast, uint32_
     int pack = 0;
     if (rbamd::tuning().pack < 0) {
         if (!f64 && rbamd::jit_fd_form(mb->model) == 2)
-            pack = B <= kSplit1MaxBatch ? 5 : B < kSplitMaxBatch ? 4 : 0;
+            pack = B <= kSplit1MaxBatch ? 5 : B <= kSplitMaxBatch ? 4 : 0;
         else  // paired lanes halve the grid: below kPackMinBatch one per lane fills more CUs
             pack = B < kPackMinBatch ? 1 : 0;
     }
@@ -342,6 +359,12 @@ hipError_t launch_crba_any(const Multibody *mb, const T *mdl, const T *q, T *H, 
 
 // fwd_kin / jac: the precompiled kernels for serial revolute chains, hipRTC kernels
 // (tree_body.hip.hpp) for trees and prismatic joints.
+// The hipRTC fwd_kin / jac kernel of a tree / prismatic model (serial revolute chains run the
+// precompiled kernels); the launchers and multibody_kernel_path_ex resolve through this one.
+const rbamd::JitKernel *jit_kin(const Multibody *mb, bool jac, bool f64) {
+    return jit_get(mb, jac ? rbamd::JitKind::Jac : rbamd::JitKind::FwdKin, f64, !f64 && fast_trig());
+}
+
 template <typename T>
 hipError_t launch_kin_any(const Multibody *mb, bool jac, const T *mdl, const T *q, T *out, uint32_t B, int64_t ld,
                           hipStream_t s) {
@@ -350,7 +373,7 @@ hipError_t launch_kin_any(const Multibody *mb, bool jac, const T *mdl, const T *
     if (mb->model.serial_revolute())
         return jac ? rbamd::launch_jac<T>(mb->model.n, mdl, q, out, B, ld, s, fast)
                    : rbamd::launch_fwd_kin<T>(mb->model.n, mdl, q, out, B, ld, s, fast);
-    const rbamd::JitKernel *jk = jit_get(mb, jac ? rbamd::JitKind::Jac : rbamd::JitKind::FwdKin, sizeof(T) == 8, fast);
+    const rbamd::JitKernel *jk = jit_kin(mb, jac, sizeof(T) == 8);
     if (!jk) return no_generic(mb);
     void *args[] = {(void *)&q, (void *)&out, (void *)&B, (void *)&ld};
     return jit_launch(jk, B, args, s);
@@ -782,29 +805,46 @@ int multibody_topology(const Multibody *mb, int *parent, int *joint_type) {
     return RB_OK;
 }
 
-int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled) {
-    if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
-    if (batch < 1) return -set_err(RB_ERR_ARG, "batch must be positive");
-    if (kind >= 4 && (!f64 || mb->model.serial_revolute())) return 0;  // precompiled fp64 kinematics
-    if (!rbamd::jit_enabled()) return 0;
-    // the same kernel resolution as the launchers (launch_*_any) for a launch of `batch`
+namespace {
+// The kernel a launch of `batch` configurations of `kind` takes: the same resolution as the
+// launchers (launch_*_any).  *generic = true when the precompiled kernel runs (serial revolute
+// fwd_kin / jac, JIT disabled or failed).
+const rbamd::JitKernel *resolve_kernel(const Multibody *mb, int kind, bool f64, int64_t batch, bool tiled) {
+    if (kind >= 4 && mb->model.serial_revolute()) return nullptr;  // precompiled kinematics
+    if (!rbamd::jit_enabled()) return nullptr;
     const uint32_t B = batch < kChunk ? (uint32_t)batch : (uint32_t)kChunk;
-    const rbamd::JitKernel *jk = nullptr;
-    if (kind == 0) {
-        jk = jit_rnea(mb, f64 != 0, fast_trig(), B, tiled != 0);
-    } else if (kind == 1) {
-        jk = jit_fd(mb, f64 != 0, fast_trig(), B);
-    } else if (kind == 3) {
-        jk = jit_rollout(mb, f64 != 0, fast_trig(), B);
-    } else {
-        jk = jit_get(mb, (rbamd::JitKind)kind, f64 != 0, kind == 2 || kind >= 4 ? false : fast_trig());
-    }
-    if (jk) return 1;
+    if (kind == 0) return jit_rnea(mb, f64, fast_trig(), B, tiled);
+    if (kind == 1) return jit_fd(mb, f64, fast_trig(), B);
+    if (kind == 3) return jit_rollout(mb, f64, fast_trig(), B);
+    if (kind >= 4) return jit_kin(mb, kind == 5, f64);
+    return jit_get(mb, rbamd::JitKind::Crba, f64, false);
+}
+
+int check_kernel_query(const Multibody *mb, int kind, int64_t batch) {
+    if (!mb) return set_err(RB_ERR_NULL, "NULL Multibody handle");
+    if (kind < 0 || kind > 5) return set_err(RB_ERR_ARG, kKindMsg);
+    if (batch < 1) return set_err(RB_ERR_ARG, "batch must be positive");
+    return RB_OK;
+}
+
+void note_jit_errors(const Multibody *mb) {
     std::lock_guard<std::mutex> lk(mb->mu);
     for (auto &kv : mb->jit)
         if (!kv.second.error.empty()) g_last_error = kv.second.error;
+}
+}  // namespace
+
+int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled) {
+    if (int rc = check_kernel_query(mb, kind, batch)) return -rc;
+    if (resolve_kernel(mb, kind, f64 != 0, batch, tiled != 0)) return 1;
+    if (rbamd::jit_enabled() && !(kind >= 4 && mb->model.serial_revolute())) note_jit_errors(mb);
     return 0;
+}
+
+int multibody_kernel_form_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled) {
+    if (int rc = check_kernel_query(mb, kind, batch)) return -rc;
+    const rbamd::JitKernel *jk = resolve_kernel(mb, kind, f64 != 0, batch, tiled != 0);
+    return jk ? jk->pack : 0;
 }
 
 int multibody_kernel_path(const Multibody *mb, int kind, int f64) {
@@ -822,7 +862,7 @@ int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int6
     if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
     if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
     const std::string src = rbamd::jit_source(mb->model, (rbamd::JitKind)kind, f64 != 0,
-                                              kind != 2 && kind < 4 && fast_trig() && !f64);
+                                              kind != 2 && fast_trig() && !f64);
     if (buf && cap > 0) {
         const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
         std::memcpy(buf, src.data(), n);
@@ -836,7 +876,7 @@ int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char
     if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
     std::vector<char> code;
     std::string err;
-    if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && kind < 4 && fast_trig() && !f64,
+    if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && fast_trig() && !f64,
                             arch ? arch : "gfx950", &code, &err))
         return -set_err(RB_ERR_HIP, err);
     return (int64_t)code.size();

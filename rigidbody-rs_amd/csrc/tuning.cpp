@@ -9,6 +9,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 
 namespace rbamd {
@@ -67,15 +68,28 @@ Tuning &tuning() {
 }
 
 namespace {
-std::atomic<unsigned> g_generation{1};
-}
+// Sequence count: even when no write is in progress; tuning_set makes it odd, stores, makes it
+// even again (writers serialised by g_write).
+std::atomic<unsigned> g_generation{2};
+std::mutex g_write;
+}  // namespace
 
 unsigned tuning_generation() { return g_generation.load(std::memory_order_acquire); }
+
+unsigned tuning_generation_stable() {
+    for (;;) {
+        const unsigned g = g_generation.load(std::memory_order_acquire);
+        if ((g & 1u) == 0) return g;
+        std::this_thread::yield();
+    }
+}
 
 int tuning_set(const char *key, int value) {
     for (const Key &k : kKeys) {
         if (std::strcmp(k.name, key) != 0) continue;
         if (k.experimental && !tuning_experimental()) return 2;
+        std::lock_guard<std::mutex> lk(g_write);
+        g_generation.fetch_add(1, std::memory_order_acq_rel);
         (tuning().*(k.field)).store(value);
         g_generation.fetch_add(1, std::memory_order_acq_rel);
         return 0;

@@ -79,9 +79,12 @@ bool tuning_experimental();
 // Sets `key`; returns 0, 1 (unknown key) or 2 (experimental key without RB_EXPERIMENTAL=1).
 int tuning_set(const char *key, int value);
 
-// Bumped by every successful tuning_set (>= 1): per-launch caches keyed on the tuning state
-// (capi.cpp jit_get's fast path) compare it instead of rebuilding their string keys.
+// Advanced twice by every successful tuning_set (odd while the write is in progress, even
+// otherwise): per-launch caches keyed on the tuning state (capi.cpp jit_get's fast path)
+// compare it instead of rebuilding their string keys.
 unsigned tuning_generation();
+// The current generation once no rb_set_tuning write is in progress (an even sequence count).
+unsigned tuning_generation_stable();
 
 // Blocks for a streaming launch of `kfn`: factor x (resident blocks per CU x CUs) on the
 // current device, never more than `full` (one block per 256 configurations).  Cached per

@@ -87,6 +87,7 @@ _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
 _sig("multibody_single_config_path", ctypes.c_int, [_vp])
 _sig("multibody_kernel_path", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int])
 _sig("multibody_kernel_path_ex", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _i64, ctypes.c_int])
+_sig("multibody_kernel_form_ex", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _i64, ctypes.c_int])
 _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
 KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3, "fwd_kin": 4, "jac": 5}
@@ -309,6 +310,15 @@ class Multibody:
         if r < 0:
             raise RigidBodyError(last_error())
         return "jit" if r == 1 else "generic"
+
+    def kernel_form(self, kind="rnea", f64=False, batch=1 << 20, tiled=False) -> int:
+        """Configurations-per-lane form of the kernel such a launch takes (rigidbody_batch.h
+        multibody_kernel_form_ex): 0 generic, 1 one per lane, 2 packed pair, 3 sequential pair,
+        4 / 5 the packed / one-per-lane wave split."""
+        r = _lib.multibody_kernel_form_ex(self._h, KINDS[kind], int(bool(f64)), int(batch), int(bool(tiled)))
+        if r < 0:
+            raise RigidBodyError(last_error())
+        return r
 
     def single_config_path(self) -> str:
         """'host' when the single-configuration queries (rnea, crba, fwd_kin, jac) run on the

@@ -770,6 +770,63 @@ def test_fd_forms_vs_oracle(dt, ffi, dev, fr3_text):
             assert fp32_fd_backward_ratio(res, Hraw, qdd, x[2]).max() <= FD32_BACKWARD_K, what
 
 
+def test_policy_forms_at_config_sizes(ffi, dev, fr3_text):
+    """The auto policy's kernel at each BASELINE config size is the form the oracle tests force,
+    bit for bit: fp32 forward dynamics at 65536 / 65539 (config 3) takes the packed wave split
+    (pack 4, fdh_split_block2) and at 2^20 the packed pair (2); at config 4's 2^17 fp64 shard the
+    RNEA and the forward dynamics take one configuration per lane (1) -- each compared with the
+    same launch under the forced form (multibody.rs:111-174 through test_fd_forms_vs_oracle /
+    test_batched_*_vs_golden)."""
+    from rigidbody_amd import chains
+
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    lim = mb.limits()
+    cases = [("fd", "f32", 65536, 4), ("fd", "f32", 65539, 4), ("fd", "f32", 1 << 20, 2),
+             ("fd", "f64", 1 << 17, 1), ("rnea", "f64", 1 << 17, 1), ("rnea", "f32", 65536, 1)]
+    for kind, dt, B, form in cases:
+        f64 = dt == "f64"
+        npd = "float64" if f64 else "float32"
+        dtype = torch.float64 if f64 else torch.float32
+        kinds = ("q", "qd", "tau") if kind == "fd" else ("q", "qd", "qdd")
+        x = [_t(chains.host_uniform(7, B, *chains.input_ranges(lim, k), chains.SEED + 70 + i, dtype=npd), dev, dtype)
+             for i, k in enumerate(kinds)]
+        call = mb.fd_batch if kind == "fd" else mb.rnea_batch
+        assert mb.kernel_path(kind, f64, B) == "jit", ffi.last_error()
+        assert mb.kernel_form(kind, f64, B) == form, (kind, dt, B, mb.kernel_form(kind, f64, B))
+        auto = call(*x).cpu().numpy()
+        try:
+            ffi.set_tuning("pack", form)
+            assert mb.kernel_form(kind, f64, B) == form
+            forced = call(*x).cpu().numpy()
+        finally:
+            ffi.set_tuning("pack", -1)
+        np.testing.assert_array_equal(auto, forced, err_msg=f"{kind} {dt} B={B}")
+
+
+def test_fd32_forms_bit_identical(ffi, dev, fr3_text):
+    """Every launch form of the fp32 mass-matrix forward dynamics (one per lane, packed pair,
+    packed / one-per-lane wave splits) runs the same fdh_bias / fdh_factor / fdh_solve code, so
+    the result does not depend on the form -- i.e. on the batch size or shard a configuration
+    lands in (the policy switches form at 2^15 / 2^17)."""
+    from rigidbody_amd import chains
+
+    mb = ffi.Multibody.from_urdf_string(fr3_text)
+    lim = mb.limits()
+    B = 65536 + 129
+    x = [_t(chains.host_uniform(7, B, *chains.input_ranges(lim, k), chains.SEED + 80 + i, dtype="float32"), dev,
+            torch.float32) for i, k in enumerate(("q", "qd", "tau"))]
+    res = {}
+    try:
+        for pack in (1, 2, 4, 5):
+            ffi.set_tuning("pack", pack)
+            assert mb.kernel_form("fd", False, B) == pack
+            res[pack] = mb.fd_batch(*x).cpu().numpy()
+    finally:
+        ffi.set_tuning("pack", -1)
+    for pack in (2, 4, 5):
+        np.testing.assert_array_equal(res[pack], res[1], err_msg=f"pack {pack} vs one per lane")
+
+
 def test_fd_mass_matrix_full_size_f64(ffi, dev, fr3_text):
     """The mass-matrix forward dynamics (fd_form 2, the FR3 default) at BASELINE config 4's
     size, B = 2^20 fp64, on every column: the fd -> rnea round trip reproduces tau to 1e-8

@@ -90,7 +90,10 @@ def test_tree_batched_f64(case, dev):
     assert np.array_equal(tau_t, mb.rnea_batch(_t(q, dev), _t(qd, dev), _t(qdd, dev)).cpu().numpy())
     qdd_t = ffi.from_tiled(mb.fd_batch_tiled(tq, tqd, ttin, B), B).cpu().numpy()
     assert np.array_equal(qdd_t, qdd_gpu)
-    # fp32 forward kinematics / Jacobian through the same hipRTC tree kernels
+    # fp32 forward kinematics / Jacobian through the same hipRTC tree kernels -- reported as such
+    # (the query resolves the kernel the launch takes, so it is built before any graph capture)
+    for kind in ("fwd_kin", "jac"):
+        assert mb.kernel_path(kind, False) == "jit" and mb.kernel_form(kind, False) == 1, ffi.last_error()
     q32 = _t(q, dev).float()
     q64 = q32.double().cpu().numpy()
     pos32 = mb.fwd_kin_batch(q32).cpu().numpy()
