@@ -2,7 +2,7 @@
 
 usage: python tools/traffic_summary.py GPURUN_OUT_DIR PROFILE_DIR WORKLOAD [KERNEL_REGEX]
 
-Reads <dir>/pmc_fetch/*counter_collection.csv, pmc_write/…, pmc_sq/…, pmc_grbm/… (one
+Reads <dir>/pmc_fetch/*counter_collection.csv, pmc_write/…, pmc_sq/…, pmc_grbm/…, pmc_flops/… (one
 rocprofv3 --pmc pass each: FETCH_SIZE costs 3 TCC slots and WRITE_SIZE 2, so they cannot
 share a pass, MI355X_MICROARCH.md "rocprofv3 PMC slots") and writes
   PROFILE_DIR/pmc_<pass>_summary.csv    per-counter mean / min / max / launches
@@ -38,7 +38,7 @@ def main():
     per = {}
     durs = []
     grbm = []
-    for p in ("fetch", "write", "sq", "grbm"):
+    for p in ("fetch", "write", "sq", "grbm", "flops"):
         v = load(os.path.join(src, f"pmc_{p}"), regex, durs if p == "grbm" else None)
         if p == "grbm":
             grbm = v.get("GRBM_GUI_ACTIVE", [])
@@ -84,6 +84,10 @@ def main():
             "note": "GRBM_GUI_ACTIVE / (End - Start) of the PMC pass's dispatches (counter summed over the "
                     "chip's GRBM instances, so a relative figure, not MHz)"}
     out["grbm_per_launch"] = {k: v for k, v in per.items() if k.startswith("GRBM_")}
+    fl = {k: v for k, v in per.items() if k.startswith("SQ_INSTS_VALU_FLOPS")}
+    if fl:
+        # gfx950 FLOP counters (pass pmc_flops): FLOPs the kernel's VALU executed per launch
+        out["valu_flops_per_launch"] = fl
     out["method"] = ("rocprofv3 --pmc passes FETCH_SIZE / WRITE_SIZE / SQ_* / GRBM_* run separately on "
                      "`bench.py --no-cpu-baseline --no-secondary`, kernels matching " + regex +
                      ", mean over the profiled launches; bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), "
