@@ -35,43 +35,21 @@ namespace dev {
 #endif
 
 // 1. bias torques C = rnea(q, qd, 0) (multibody.rs:111-153 with ddq = 0); also the joint
-// (cos, sin) the later stages reuse.
-// Model-specialised kernels whose R_p are signed permutations (RB_SPLIT_ROT) with centre-of-mass
-// link forces run the backward sweep (multibody.rs:143-150) in a fused form: the forward sweep
-// leaves each link's force as g = f / m (link_force_g), and each step computes the parent's
-// transmitted force as F_{j-1} = m_{j-1} g_{j-1} + E_j F_j and its moment as
-// n_{j-1} + E_j n_j + p_j x (E_j F_j) -- the link force's scaling and both accumulations become
-// FMAs with the child's terms as addends (E = R_p Rz(q) has two (cos, sin) rows and one +-e_z row
-// when R_p is a signed permutation).  FR3 fp64: 5 fewer VALU per link (tools/fd_stages.py).
+// (cos, sin) the later stages reuse.  Model-specialised kernels with signed-permutation R_p and
+// centre-of-mass link forces take the fused backward sweep (rnea_body.hip.hpp rnea_bwd_g: the
+// link force's mass scaling and the child accumulations as FMAs; FR3 fp64 5 fewer VALU per link).
 template <typename T, int N, bool FAST>
 RB_HD void fdh_bias(const T *mdl, const T (&qv)[N], const T (&qdv)[N], T (&cs)[N], T (&sn)[N], T (&C)[N]) {
-#if RB_COM_FORM
-    constexpr bool kG = RB_SPLIT_ROT != 0;
-#else
-    constexpr bool kG = false;
-#endif
-    V3<T> fn[N], ff[N];  // ff: the link force, or g = f / m (kG)
+    V3<T> fn[N], ff[N];  // ff: the link force, or g = f / m (kRneaGForm)
     RneaState<T> st;
-    rnea_fwd0<T, FAST, kG>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0]);
+    rnea_fwd0<T, FAST, kRneaGForm>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0]);
 #pragma unroll
-    for (int j = 1; j < N; ++j) rnea_fwd<T, FAST, kG>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j]);
+    for (int j = 1; j < N; ++j)
+        rnea_fwd<T, FAST, kRneaGForm>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j]);
     reload_fence();
     RB_STAGE("bias_bwd");
-    if constexpr (kG) {
-        const T ml = load_link(mdl, N - 1).m;
-        V3<T> F = v3(ml * ff[N - 1].x, ml * ff[N - 1].y, ml * ff[N - 1].z);
-        V3<T> n = fn[N - 1];
-#pragma unroll
-        for (int j = N - 1; j >= 1; --j) {
-            C[j] = n.z;
-            const Link<T> L = load_link(mdl, j);
-            const M3<T> E = joint_rotation(L.Rp, cs[j], sn[j]);
-            const V3<T> fl = mul(E, F);
-            const T mp = load_link(mdl, j - 1).m;
-            F = v3(fmadd(mp, ff[j - 1].x, fl.x), fmadd(mp, ff[j - 1].y, fl.y), fmadd(mp, ff[j - 1].z, fl.z));
-            n = cross_add(mul_add(fn[j - 1], E, n), L.p, fl);
-        }
-        C[0] = n.z;
+    if constexpr (kRneaGForm) {
+        rnea_bwd_g<T, N>(mdl, cs, sn, fn, ff, [&](int j, T v) { C[j] = v; });
     } else {
 #pragma unroll
         for (int j = N - 1; j >= 1; --j) {

@@ -82,6 +82,38 @@ RB_HD void rnea_bwd(const T *mdl, int j, T cj, T sj, const V3<T> &ffj, const V3<
     fnp = cross_add(mul_add(fnp, Rp, zn), p, fl);
 }
 
+// Backward sweep over link forces left unscaled by the forward sweep (link_force_g: n_j and
+// g_j = f_j / m_j), for model-specialised kernels whose R_p are signed permutations
+// (RB_SPLIT_ROT) with centre-of-mass link forces: each step forms the parent's transmitted force
+// F_{j-1} = m_{j-1} g_{j-1} + E_j F_j and moment n_{j-1} + E_j n_j + p_j x (E_j F_j)
+// (multibody.rs:143-150), so the link force's scaling and both accumulations are FMAs with the
+// child's terms as addends (E = R_p Rz(q) has two (cos, sin) rows and one +-e_z row).
+// tau_j = n_j.z (multibody.rs:144) goes to out(j, value), leaf first.
+#if RB_COM_FORM
+constexpr bool kRneaGForm = RB_SPLIT_ROT != 0;
+#else
+constexpr bool kRneaGForm = false;
+#endif
+
+template <typename T, int N, typename Out>
+RB_HD void rnea_bwd_g(const T *mdl, const T (&cs)[N], const T (&sn)[N], const V3<T> (&fn)[N], const V3<T> (&g)[N],
+                      Out &&out) {
+    const T ml = load_link(mdl, N - 1).m;
+    V3<T> F = v3(ml * g[N - 1].x, ml * g[N - 1].y, ml * g[N - 1].z);
+    V3<T> n = fn[N - 1];
+#pragma unroll
+    for (int j = N - 1; j >= 1; --j) {
+        out(j, n.z);
+        const Link<T> L = load_link(mdl, j);
+        const M3<T> E = joint_rotation(L.Rp, cs[j], sn[j]);
+        const V3<T> fl = mul(E, F);
+        const T mp = load_link(mdl, j - 1).m;
+        F = v3(fmadd(mp, g[j - 1].x, fl.x), fmadd(mp, g[j - 1].y, fl.y), fmadd(mp, g[j - 1].z, fl.z));
+        n = cross_add(mul_add(fn[j - 1], E, n), L.p, fl);
+    }
+    out(0, n.z);
+}
+
 // Forward sweep (multibody.rs:122-141) then backward sweep (143-150), fused: the
 // per-link forces never leave registers.  One call evaluates the configuration whose
 // joint values are in (qv, qdv, qddv) and hands tau_j to `out(j, value)`.
@@ -89,14 +121,19 @@ template <typename T, int N, bool FAST, typename Out>
 RB_HD void rnea_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
                                           const T (&qddv)[N], Out &&out) {
     T cs[N], sn[N];
-    V3<T> fn[N], ff[N];  // per-link spatial force: moment n (rot), force f (lin)
+    V3<T> fn[N], ff[N];  // per-link spatial force: moment n (rot), force f (lin) -- or g = f / m
     RneaState<T> st;
-    rnea_fwd0<T, FAST>(mdl, qv[0], qdv[0], qddv[0], st, sn[0], cs[0], fn[0], ff[0]);
+    rnea_fwd0<T, FAST, kRneaGForm>(mdl, qv[0], qdv[0], qddv[0], st, sn[0], cs[0], fn[0], ff[0]);
 #pragma unroll
-    for (int j = 1; j < N; ++j) rnea_fwd<T, FAST>(mdl, j, qv[j], qdv[j], qddv[j], st, sn[j], cs[j], fn[j], ff[j]);
+    for (int j = 1; j < N; ++j)
+        rnea_fwd<T, FAST, kRneaGForm>(mdl, j, qv[j], qdv[j], qddv[j], st, sn[j], cs[j], fn[j], ff[j]);
 
     // Backward sweep: tau_i = n_i.z (multibody.rs:144)
     reload_fence();
+    if constexpr (kRneaGForm) {
+        rnea_bwd_g<T, N>(mdl, cs, sn, fn, ff, static_cast<Out &&>(out));
+        return;
+    }
 #pragma unroll
     for (int j = N - 1; j >= 1; --j) {
         out(j, fn[j].z);
