@@ -29,6 +29,12 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 METRIC = "RNEA evals/sec (fr3 7-DOF, batch 2^20) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK = 8.0e12  # B/s, MI355X spec (/opt/skills/guides/MI355X_MICROARCH.md)
+# VALU roofline: 256 CUs x 4 SIMDs, 2.4 GHz peak engine clock; vector FLOP peaks
+# fp32 157.3 TF (MI355X_MICROARCH.md), fp64 78.6 TF (AMD spec: half the fp32 lanes -- the measured
+# 4-cycle wave64 v_fma_f64 issue, 16 lanes/clk/SIMD)
+SIMDS = 1024
+CLOCK_PEAK = 2.4e9
+VALU_FLOP_PEAK = {"f32": 157.3e12, "f64": 78.6e12}
 
 
 def parse(argv=None):
@@ -443,7 +449,15 @@ def side_workloads(mb7, a):
                      "launches": r["steps"],
                      "layout": layout, "dtype": dt_name, "hbm_frac": r["bytes"] / (r["kernel_ms_avg"] * 1e-3) / HBM_PEAK,
                      "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64", B, layout == "tiled")
+                                             for k in kernel.split("_")),
+                     "kernel_form": "+".join(str(mb.kernel_form(k, dt_name == "f64", B, layout == "tiled"))
                                              for k in kernel.split("_"))}
+        if kernel in ("rnea", "fd"):
+            model = "fr3" if mb.n == 7 else f"chain{mb.n}" if "tree" not in name else None
+            if model:
+                sec[name]["valu"] = valu_roofline(workload_name(kernel, mb.n, dt_name, layout, B), f"{kernel}_{model}",
+                                                  f"{kernel}_{model}_{dt_name}" + ("" if B == a.batch else f"_b{B}"),
+                                                  dt_name, B, r["kernel_ms_avg"])
         if graph:  # the same launches replayed from a HIP graph; rates over the launches replayed
             gl = r["graph_launches"]
             # eager back-to-back launches from Python are host-bound when the graph replay of the
@@ -485,7 +499,9 @@ def side_workloads(mb7, a):
         sec[f"rollout_fr3_{dn}_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
                                         "launches": nl,
                                         "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", dn == "f64"),
-                                        "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)"}
+                                        "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)",
+                                        "valu": valu_roofline(f"rollout_fr3_{dn}_K16_b{a.batch}", "rollout_step_fr3",
+                                                              f"rollout_fr3_{dn}", dn, a.batch * K, km)}
     # the MPC-sized rollout (65536 configurations, K = 16): the split of packed waves per step
     # (rollout_split_block2), device-bound rate from a HIP graph
     Bs = 65536
@@ -610,6 +626,63 @@ def load_traffic(workload):
     return None
 
 
+def _load_json(rel):
+    path = os.path.join(REPO, rel)
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def held_clock(name):
+    """Median in-kernel shader clock (GHz) of kernel `name` under sustained load, from the
+    committed clock probe (tools/clock_probe.py, profiles/r04/clock_probe.jsonl), or None."""
+    path = os.path.join(REPO, "profiles", "r04", "clock_probe.jsonl")
+    if not os.path.exists(path):
+        return None
+    for ln in open(path):
+        if ln.strip().startswith("{"):
+            d = json.loads(ln)
+            if d.get("kernel") == name:
+                return d.get("clock_GHz_median")
+    return None
+
+
+def valu_roofline(workload, op_key, clock_key, dt_name, evals, kern_ms):
+    """roofline.valu for a VALU-heavy kernel (SURVEY §8(d) "reported alongside"): the committed
+    PMC counters of this workload's kernel (profiles/traffic_<workload>.json) over this run's
+    kernel time.  issue_frac = SIMD cycles of VALU issue (SQ_ACTIVE_INST_VALU, quad-cycles x 4,
+    summed over waves) / (1024 SIMDs x clock x kernel time), at 2.4 GHz and at the clock the chip
+    holds under this kernel (clock probe); flop_frac = VALU FLOPs executed (gfx950
+    SQ_INSTS_VALU_FLOPS_*) / the dtype's vector peak; flops_per_eval_ref = the reference
+    formulation's operations per evaluation (op-counting oracle build, profiles/r04/op_counts.json)."""
+    tr = load_traffic(workload)
+    ops = _load_json("profiles/r04/op_counts.json")
+    t = kern_ms * 1e-3
+    out = {"bound": "valu", "unit": "fraction", "evals_per_launch": evals}
+    if ops and op_key in ops:
+        ref = ops[op_key]["flops"]
+        out.update({"flops_per_eval_ref": ref, "ref_equiv_tflops": ref * evals / t / 1e12,
+                    "ref_source": f"profiles/r04/op_counts.json [{op_key}] (oracle/flops.cpp)"})
+    sq = (tr or {}).get("sq_counters_per_launch", {})
+    if "SQ_INSTS_VALU" in sq and "SQ_ACTIVE_INST_VALU" in sq:
+        busy = sq["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS  # VALU issue cycles per SIMD per launch
+        out.update({"insts_per_eval": sq["SQ_INSTS_VALU"] / evals,
+                    "issue_cycles_per_eval": sq["SQ_ACTIVE_INST_VALU"] * 4 / evals,
+                    "issue_frac_2p4ghz": busy / (CLOCK_PEAK * t)})
+        clk = held_clock(clock_key)
+        if clk:
+            out.update({"held_clock_ghz": clk, "issue_frac_held": busy / (clk * 1e9 * t),
+                        "clock_source": f"profiles/r04/clock_probe.jsonl [{clock_key}]"})
+        fl = tr.get("valu_flops_per_launch", {})
+        kf = sum(v for k, v in fl.items() if dt_name.upper()[1:] in k)  # FP32 / FP64 (+ _TRANS)
+        if kf:
+            out.update({"kernel_flops_per_eval": kf / evals, "kernel_tflops": kf / t / 1e12,
+                        "flop_frac": kf / t / VALU_FLOP_PEAK[dt_name], "flop_peak_tflops": VALU_FLOP_PEAK[dt_name] / 1e12})
+        out["counters_source"] = f"profiles/traffic_{workload}.json (rocprofv3 PMC passes of this kernel)"
+    return out
+
+
 def workload_name(kernel, n, dt_name, layout, B):
     return f"{kernel}_{'fr3' if n == 7 else f'chain{n}'}_{dt_name}_{layout}_b{B}"
 
@@ -677,6 +750,10 @@ def main(a):
     }
     if traffic:
         line["roofline"]["traffic_source"] = f"profiles/traffic_{workload}.json (rocprofv3 PMC passes)"
+    if not a.stub:
+        model = "fr3" if n == 7 else f"chain{n}"
+        line["roofline"]["valu"] = valu_roofline(workload, f"{a.kernel.split('_')[0]}_{model}",
+                                                 f"{a.kernel}_{model}_{a.dtype}", a.dtype, B, kern_ms)
     if world > 1:
         line["per_rank"] = ranks
     sec = {}
