@@ -293,6 +293,11 @@ unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
         const unsigned P = (T - S) & ~1u;
         return P / 2u + (T - P);
     }
+    if (jk->pack == 6) {  // resident grid of one-wave blocks over 64-configuration chunks
+        const unsigned chunks = (unsigned)(((uint64_t)B + 63u) / 64u);
+        const unsigned r = jk->resident > 0 ? jk->resident : 1u;
+        return chunks < r ? chunks : r;
+    }
     // pack 2 / 3: two configurations per lane; pack 5: the one-per-lane wave split, 128 per block
     // (pack 4, the packed split, covers 256 per block like one per lane)
     const unsigned per_block = jk->pack == 5 ? 128u : 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
@@ -300,7 +305,7 @@ unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
 }
 
 hipError_t jit_launch(const rbamd::JitKernel *jk, uint32_t B, void **args, hipStream_t s) {
-    return hipModuleLaunchKernel(jk->function, jit_grid(jk, B), 1, 1, 256u, 1, 1, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(jk->function, jit_grid(jk, B), 1, 1, jk->block, 1, 1, 0, s, args, nullptr);
 }
 
 // tiled: the [ceil(B/256)][n][256] layout (kernels.hpp); the JIT lane kernels and the

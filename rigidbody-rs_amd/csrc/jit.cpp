@@ -80,7 +80,10 @@ int jit_pack(JitKind kind, bool f64, int n) {
     // fp64 RNEA of chains up to 8 links: 125 VGPRs, still 4 waves/SIMD; FR3 2^20 tiled
     // 42.0-42.8 us steady where the one-per-lane kernel alternates between ~40.7 and ~48.8 us
     // phases, mean 44.3-44.6).
+    // 6 = resident grid of one-wave blocks with the next chunk's inputs staged in LDS by direct
+    // global->LDS loads (rnea_body.hip.hpp rnea_resident_lds: fp32 RNEA of long chains).
     const int v = tuning().pack;
+    if (v == 6) return (kind == JitKind::Rnea && !f64) ? 6 : 1;
     if (kind == JitKind::Rollout) return ((v < 0 || v == 2 || v == 4) && !f64 && n <= 8) ? (v == 4 ? 4 : 2) : 1;
     if (kind != JitKind::Fd && kind != JitKind::Rnea) return 1;
     if (v == 3) return 3;
@@ -120,6 +123,7 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
         return (!f64 && m.n <= 8) ? 2 : 1;  // the split needs the mass-matrix form: the pair instead
     if ((pack == 4 || pack == 5) && kind != JitKind::Rollout && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2))
         return 1;
+    if (pack == 6 && !(kind == JitKind::Rnea && !f64 && m.serial_revolute())) return 1;
     return pack;
 }
 
@@ -275,7 +279,12 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     const char *head = head_s.c_str();
     // Lane kernels take the block stride bs (elements): 256 for SoA, N * 256 for the tiled
     // layout (kernels.hpp); block k's arrays start at element k * bs, lane offset threadIdx.x.
-    if (kind == JitKind::Rnea && pack == 3 && tail > 0) {
+    if (kind == JitKind::Rnea && pack == 6) {
+        o << "extern \"C\" __global__ __launch_bounds__(64) void rb_jit_kernel(const T *__restrict__ q, "
+             "const T *__restrict__ qd, const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, "
+             "int64_t bs) {\n";
+        o << "  rbamd::dev::rnea_resident_lds<T, N, " << F << ">(kModel, q, qd, qdd, tau, B, ld, bs);\n}\n";
+    } else if (kind == JitKind::Rnea && pack == 3 && tail > 0) {
         // pairs of tiles for blocks < G1, then one tile per block for the last S tiles
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
@@ -392,6 +401,10 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
         optv.push_back("-mllvm");
         optv.push_back("-disable-machine-licm");
     }
+    // The resident-grid RNEA (pack 6): inside its chunk loop the SLP vectorizer pairs the fp32
+    // recursion into v_pk ops whose register pairs push the 30-link kernel to 256 VGPRs + 242
+    // AGPRs (1 wave/SIMD); without it 243 VGPRs, 2 waves/SIMD like the one-chunk kernel.
+    if (src.find("rnea_resident_lds") != std::string::npos) optv.push_back("-fno-slp-vectorize");
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)optv.size(), optv.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
@@ -450,6 +463,14 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack,
         jk.module = nullptr;
         jk.function = nullptr;
         return jk;
+    }
+    if (jk.pack == 6) {  // persistent grid: every block resident at once
+        jk.block = 64;
+        int per_cu = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jk.function, (int)jk.block, 0) != hipSuccess ||
+            per_cu < 1)
+            per_cu = 1;
+        jk.resident = (unsigned)per_cu * (unsigned)(prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256);
     }
     return jk;
 }

@@ -281,6 +281,49 @@ def test_chain30_full_size_f32(ffi, dev):
           f"affine {worst_aff:.2e}, fd32 backward K {K:.1f}")
 
 
+@pytest.mark.parametrize("model", ["chain30", "fr3"])
+def test_resident_lds_rnea_bit_identical(model, ffi, dev, fr3_text):
+    """The resident-grid RNEA with LDS-staged inputs (jit pack 6, rnea_body.hip.hpp
+    rnea_resident_lds: one-wave blocks walking 64-configuration chunks, the next chunk's rows
+    loaded straight into LDS during the current one's dynamics) is the same per-lane
+    arithmetic as the one-per-lane kernel: bit-identical on ragged batches (a partial last
+    chunk, batches larger and smaller than the resident grid), SoA with ld > B (padding
+    untouched) and tiled; oracle spot columns (multibody.rs:111-153, fp32 1e-4)."""
+    from rigidbody_amd import chains
+
+    xml = chains.synthetic_chain_urdf(30) if model == "chain30" else fr3_text
+    mb = ffi.Multibody.from_urdf_string(xml)
+    om = _oracle(xml)
+    n, lim = mb.n, mb.limits()
+    for B in (1, 63, 65, 1000, 300007):
+        ld = B + 5
+        full = [torch.full((n, ld), 7.0, dtype=torch.float32, device=dev) for _ in range(3)]
+        for k, kind in enumerate(("q", "qd", "qdd")):
+            full[k][:, :B] = _t(chains.host_uniform(n, B, *chains.input_ranges(lim, kind), chains.SEED + 90 + k,
+                                                    dtype="float32"), dev, torch.float32)
+        x = [f[:, :B] for f in full]
+        res = {}
+        try:
+            for pack in (1, 6):
+                ffi.set_tuning("pack", pack)
+                assert mb.kernel_form("rnea", False, B) == pack
+                out = torch.full((n, ld), 123.0, dtype=torch.float32, device=dev)
+                mb.rnea_batch(*x, out=out[:, :B])
+                assert torch.all(out[:, B:] == 123.0), (B, pack)
+                til = ffi.from_tiled(mb.rnea_batch_tiled(*[ffi.to_tiled(a.contiguous()) for a in x], B), B)
+                res[pack] = (out[:, :B].cpu().numpy(), til.cpu().numpy())
+        finally:
+            ffi.set_tuning("pack", -1)
+        np.testing.assert_array_equal(res[6][0], res[1][0], err_msg=f"{model} B={B} soa")
+        np.testing.assert_array_equal(res[6][1], res[1][1], err_msg=f"{model} B={B} tiled")
+        np.testing.assert_array_equal(res[6][0], res[6][1], err_msg=f"{model} B={B} soa vs tiled")
+        idx = np.unique(np.linspace(0, B - 1, min(B, 256)).astype(int))
+        xs = [a[:, idx].double().cpu().numpy() for a in x]
+        ref = om.rnea_batch(*xs)
+        got = res[6][0][:, idx].astype(np.float64)
+        assert (np.abs(got - ref).max(0) / (1 + np.abs(ref).max(0))).max() <= 1e-4, (model, B)
+
+
 def test_full_size_properties(ffi, dev, fr3_text):
     """BASELINE config size (fr3, B = 2^20): the oracle cannot cover every column, so
     check size-independent properties on all of them plus an oracle spot check:
