@@ -575,8 +575,8 @@ Multibody *new_from_text(const std::string &xml, unsigned flags = 0) {
 }  // namespace
 
 namespace {
-template <typename Launch>
-int host_batch(const Multibody *mb, const double *const *in, int nin, double *out, int64_t batch, Launch launch) {
+template <typename T, typename Launch>
+int host_batch(const Multibody *mb, const T *const *in, int nin, T *out, int64_t batch, Launch launch) {
     int rc = check_batch(mb, batch, batch);
     if (rc) return rc;
     if (batch == 0) return RB_OK;
@@ -584,18 +584,18 @@ int host_batch(const Multibody *mb, const double *const *in, int nin, double *ou
         if (!in[k]) return set_err(RB_ERR_NULL, "NULL array");
     if (!out) return set_err(RB_ERR_NULL, "NULL array");
     const size_t per = (size_t)mb->model.n * (size_t)batch;
-    double *d = nullptr;
+    T *d = nullptr;
     hipStream_t s = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_err(e, "hipStreamCreate");
-    e = hipMallocAsync((void **)&d, per * (nin + 1) * sizeof(double), s);
+    e = hipMallocAsync((void **)&d, per * (nin + 1) * sizeof(T), s);
     if (e != hipSuccess) { (void)hipStreamDestroy(s); return hip_err(e, "hipMallocAsync"); }
     for (int k = 0; k < nin && e == hipSuccess; ++k)
-        e = hipMemcpyAsync(d + k * per, in[k], per * sizeof(double), hipMemcpyHostToDevice, s);
+        e = hipMemcpyAsync(d + k * per, in[k], per * sizeof(T), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) rc = launch(d, d + nin * per, s);
     else rc = hip_err(e, "hipMemcpyAsync H2D");
     if (rc == RB_OK) {
-        e = hipMemcpyAsync(out, d + nin * per, per * sizeof(double), hipMemcpyDeviceToHost, s);
+        e = hipMemcpyAsync(out, d + nin * per, per * sizeof(T), hipMemcpyDeviceToHost, s);
         if (e != hipSuccess) rc = hip_err(e, "hipMemcpyAsync D2H");
     }
     (void)hipFreeAsync(d, s);
@@ -603,6 +603,24 @@ int host_batch(const Multibody *mb, const double *const *in, int nin, double *ou
     if (rc == RB_OK && e != hipSuccess) rc = hip_err(e, "hipStreamSynchronize");
     (void)hipStreamDestroy(s);
     return rc;
+}
+// Blocking host-pointer forms: SoA rows x[j * batch + b] in host memory, copied to a scratch
+// device buffer on a private stream, evaluated by the batched kernels, copied back.
+template <typename T>
+int rnea_host(const Multibody *mb, const T *q, const T *qd, const T *qdd, T *tau, int64_t batch) {
+    const T *in[3] = {q, qd, qdd};
+    return host_batch<T>(mb, in, 3, tau, batch, [&](T *d, T *o, hipStream_t s) {
+        const size_t per = (size_t)mb->model.n * (size_t)batch;
+        return rnea_batch<T>(mb, d, d + per, d + 2 * per, o, batch, batch, s);
+    });
+}
+template <typename T>
+int fd_host(const Multibody *mb, const T *q, const T *qd, const T *tau, T *qdd, int64_t batch) {
+    const T *in[3] = {q, qd, tau};
+    return host_batch<T>(mb, in, 3, qdd, batch, [&](T *d, T *o, hipStream_t s) {
+        const size_t per = (size_t)mb->model.n * (size_t)batch;
+        return fd_batch<T>(mb, d, d + per, d + 2 * per, o, batch, batch, s);
+    });
 }
 }  // namespace
 
@@ -1012,20 +1030,19 @@ int multibody_jac_batch_f32(const Multibody *mb, const float *q, float *J, int64
 
 int multibody_rnea_batch_host_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
                                   double *tau, int64_t batch) {
-    const double *in[3] = {q, qd, qdd};
-    return host_batch(mb, in, 3, tau, batch, [&](double *d, double *o, hipStream_t s) {
-        const size_t per = (size_t)mb->model.n * (size_t)batch;
-        return rnea_batch<double>(mb, d, d + per, d + 2 * per, o, batch, batch, s);
-    });
+    return rnea_host<double>(mb, q, qd, qdd, tau, batch);
 }
-
 int multibody_fd_batch_host_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
                                 double *qdd, int64_t batch) {
-    const double *in[3] = {q, qd, tau};
-    return host_batch(mb, in, 3, qdd, batch, [&](double *d, double *o, hipStream_t s) {
-        const size_t per = (size_t)mb->model.n * (size_t)batch;
-        return fd_batch<double>(mb, d, d + per, d + 2 * per, o, batch, batch, s);
-    });
+    return fd_host<double>(mb, q, qd, tau, qdd, batch);
+}
+int multibody_rnea_batch_host_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                  float *tau, int64_t batch) {
+    return rnea_host<float>(mb, q, qd, qdd, tau, batch);
+}
+int multibody_fd_batch_host_f32(const Multibody *mb, const float *q, const float *qd, const float *tau,
+                                float *qdd, int64_t batch) {
+    return fd_host<float>(mb, q, qd, tau, qdd, batch);
 }
 
 // ------------------------------------------------------------- synthetic inputs

@@ -83,6 +83,9 @@ _sig("multibody_fwd_kin_batch_f32", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _v
 _sig("multibody_jac_batch_f32", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_jac_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_rnea_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
+_fp = ctypes.POINTER(ctypes.c_float)
+_sig("multibody_rnea_batch_host_f32", ctypes.c_int, [_vp, _fp, _fp, _fp, _fp, _i64])
+_sig("multibody_fd_batch_host_f32", ctypes.c_int, [_vp, _fp, _fp, _fp, _fp, _i64])
 _sig("multibody_rnea_kernel_path", ctypes.c_int, [_vp, ctypes.c_int])
 _sig("multibody_single_config_path", ctypes.c_int, [_vp])
 _sig("multibody_kernel_path", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int])
@@ -178,8 +181,10 @@ def _one_device(ts):
 
 
 def _host_soa(arrs, n):
-    """[n, B] float64 host arrays of one batched host call: same shape, n rows."""
-    out = [np.ascontiguousarray(x, dtype=np.float64) for x in arrs]
+    """[n, B] host arrays of one batched host call: same shape, n rows; float32 if every input
+    is float32 (the *_host_f32 entry points), float64 otherwise."""
+    dt = np.float32 if all(np.asarray(x).dtype == np.float32 for x in arrs) else np.float64
+    out = [np.ascontiguousarray(x, dtype=dt) for x in arrs]
     for a in out:
         if a.ndim != 2 or a.shape[0] != n or a.shape != out[0].shape:
             raise ValueError(f"host batch arrays must all be [{n}, B], got {[x.shape for x in out]}")
@@ -497,19 +502,22 @@ class Multibody:
 
     # -------------------------------------------------------- batched, host [n, B]
     def rnea_batch_host(self, q, qd, qdd):
-        arrs = _host_soa((q, qd, qdd), self.n)
-        B = arrs[0].shape[1]
-        out = np.empty_like(arrs[0])
-        _check(_lib.multibody_rnea_batch_host_f64(self._h, *[a.ctypes.data_as(_dp) for a in arrs],
-                                                  out.ctypes.data_as(_dp), B), "rnea_batch_host")
-        return out
+        """Blocking host form (multibody_rnea_batch_host_f32 / _f64 by the inputs' dtype)."""
+        return self._host_call("rnea", (q, qd, qdd))
 
     def fd_batch_host(self, q, qd, tau):
-        arrs = _host_soa((q, qd, tau), self.n)
+        """Blocking host form (multibody_fd_batch_host_f32 / _f64 by the inputs' dtype)."""
+        return self._host_call("fd", (q, qd, tau))
+
+    def _host_call(self, kind, ins):
+        arrs = _host_soa(ins, self.n)
         B = arrs[0].shape[1]
         out = np.empty_like(arrs[0])
-        _check(_lib.multibody_fd_batch_host_f64(self._h, *[a.ctypes.data_as(_dp) for a in arrs],
-                                                out.ctypes.data_as(_dp), B), "fd_batch_host")
+        f32 = arrs[0].dtype == np.float32
+        fn = getattr(_lib, f"multibody_{kind}_batch_host_{'f32' if f32 else 'f64'}")
+        ptr = _fp if f32 else _dp
+        _check(fn(self._h, *[a.ctypes.data_as(ptr) for a in arrs], out.ctypes.data_as(ptr), B),
+               f"{kind}_batch_host")
         return out
 
 

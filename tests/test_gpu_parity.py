@@ -906,3 +906,38 @@ def test_fd_mass_matrix_full_size_f64(ffi, dev, fr3_text):
         assert (err <= 1e-9 * np.maximum(1.0, cond / 1e3)).all(), (form, err.max(), cond.max())
     d = ((got[2] - got[1]).abs() / (1 + got[1].abs())).max().item()
     print(f"fd mass-matrix f64 2^20: round trip {rt:.2e}, vs ABA {d:.2e}")
+
+
+# ------------------------------------------------------------ host-pointer batched forms
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float64", "float32"])
+def test_host_batch_forms(ffi, dev, fr3_text, dtype):
+    """multibody_{rnea,fd}_batch_host_{f64,f32} (blocking, host SoA arrays): bit-identical to
+    the device-pointer entry points on the same inputs (same kernels), and the oracle's
+    tolerance (fp64 1e-9; fp32 inputs rounded to fp32, then 1e-4 scaled) on a ragged batch."""
+    from rigidbody_amd import chains
+
+    mb = ffi.Multibody.new()
+    lim = mb.limits()
+    om = _oracle(fr3_text)
+    B = 4099
+    tdt = torch.float64 if dtype == "float64" else torch.float32
+    x = {k: chains.host_uniform(7, B, *chains.input_ranges(lim, k), chains.SEED + 120 + i, dtype=dtype)
+         for i, k in enumerate(("q", "qd", "qdd", "tau"))}
+    tau_h = mb.rnea_batch_host(x["q"], x["qd"], x["qdd"])
+    qdd_h = mb.fd_batch_host(x["q"], x["qd"], x["tau"])
+    assert tau_h.dtype == np.dtype(dtype) and qdd_h.dtype == np.dtype(dtype)
+    t = {k: _t(v, dev, tdt) for k, v in x.items()}
+    tau_d = mb.rnea_batch(t["q"], t["qd"], t["qdd"]).cpu().numpy()
+    qdd_d = mb.fd_batch(t["q"], t["qd"], t["tau"]).cpu().numpy()
+    np.testing.assert_array_equal(tau_h, tau_d)
+    np.testing.assert_array_equal(qdd_h, qdd_d)
+    x64 = {k: v.astype(np.float64) for k, v in x.items()}
+    ref = om.rnea_batch(x64["q"], x64["qd"], x64["qdd"])
+    _close(tau_h, ref, 1e-9 if dtype == "float64" else 1e-4, f"host rnea {dtype}")
+    res = om.rnea_batch(x64["q"], x64["qd"], qdd_h.astype(np.float64)) - x64["tau"]
+    if dtype == "float64":  # torque residual of the solve, as test_fd_forms_vs_oracle
+        assert (np.abs(res) / (1 + np.abs(x64["tau"]))).max() <= 1e-8
+    else:  # backward error of the fp32 solve (FD32_BACKWARD_K, above)
+        K = fp32_fd_backward_ratio(res, om.crba_batch(x64["q"]), qdd_h.astype(np.float64), x64["tau"])
+        assert K.max() <= FD32_BACKWARD_K, K.max()
