@@ -675,7 +675,9 @@ def valu_roofline(workload, op_key, clock_key, dt_name, evals, kern_ms):
             out.update({"held_clock_ghz": clk, "issue_frac_held": busy / (clk * 1e9 * t),
                         "clock_source": f"profiles/r04/clock_probe.jsonl [{clock_key}]"})
         fl = tr.get("valu_flops_per_launch", {})
-        kf = sum(v for k, v in fl.items() if dt_name.upper()[1:] in k)  # FP32 / FP64 (+ _TRANS)
+        # the SQ_INSTS_VALU_FLOPS_* counters count per wave-instruction (an FMA 2, a packed FMA 4):
+        # x 64 lanes for the FLOPs executed, as rocprof-compute's VALU FLOP metric
+        kf = 64 * sum(v for k, v in fl.items() if dt_name.upper()[1:] in k)  # FP32 / FP64 (+ _TRANS)
         if kf:
             out.update({"kernel_flops_per_eval": kf / evals, "kernel_tflops": kf / t / 1e12,
                         "flop_frac": kf / t / VALU_FLOP_PEAK[dt_name], "flop_peak_tflops": VALU_FLOP_PEAK[dt_name] / 1e12})

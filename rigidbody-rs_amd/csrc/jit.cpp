@@ -82,6 +82,8 @@ int jit_pack(JitKind kind, bool f64, int n) {
     // phases, mean 44.3-44.6).
     // 6 = resident grid of one-wave blocks with the next chunk's inputs staged in LDS by direct
     // global->LDS loads (rnea_body.hip.hpp rnea_resident_lds: fp32 RNEA of long chains).
+    // 7 = the mass-matrix forward dynamics on a resident grid of 4-wave blocks, each wave's
+    // next chunk of q, qd rows staged in LDS the same way (fdh_body.hip.hpp fdh_resident_lds).
     const int v = tuning().pack;
     if (v == 6) return (kind == JitKind::Rnea && !f64) ? 6 : 1;
     if (kind == JitKind::Rollout) return ((v < 0 || v == 2 || v == 4) && !f64 && n <= 8) ? (v == 4 ? 4 : 2) : 1;
@@ -89,6 +91,8 @@ int jit_pack(JitKind kind, bool f64, int n) {
     if (v == 3) return 3;
     if (v == 4) return (kind == JitKind::Fd && !f64) ? 4 : 1;  // split packed waves (fdh_split_block2)
     if (v == 5) return (kind == JitKind::Fd && !f64) ? 5 : 1;  // split waves, one per lane (fdh_split_block1)
+    if (v == 7) return kind == JitKind::Fd ? 7 : 1;  // resident grid, LDS-staged rows (fdh_resident_lds)
+    if (v == 8) return kind == JitKind::Fd ? 8 : 1;  // one per lane in one-wave blocks
     if (v >= 0) return (v >= 2 && !f64 && kind == JitKind::Fd) ? 2 : 1;
     if (kind == JitKind::Rnea) return (f64 && n <= 8) ? 3 : 1;
     return (!f64 && n <= 8) ? 2 : 1;
@@ -124,6 +128,8 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
     if ((pack == 4 || pack == 5) && kind != JitKind::Rollout && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2))
         return 1;
     if (pack == 6 && !(kind == JitKind::Rnea && !f64 && m.serial_revolute())) return 1;
+    // 7 = the resident-grid mass-matrix FD with LDS-staged rows (one configuration per lane)
+    if ((pack == 7 || pack == 8) && !(kind == JitKind::Fd && jit_fd_form(m) == 2)) return 1;
     return pack;
 }
 
@@ -314,9 +320,18 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
         o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n}\n";
     } else if (kind == JitKind::Fd) {
-        o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+        // pack 8: one-wave blocks, so a wave slot that frees is refilled by the next wave alone
+        o << (fdh && pack == 8 ? head_s.replace(head_s.find("(256)"), 5, "(64)").c_str() : head) << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
-        if (fdh && pack == 5) {
+        if (fdh && pack == 8) {
+            o << "  const uint32_t b = blockIdx.x * 64u + threadIdx.x;\n";
+            o << "  if (b >= B) return;\n";
+            o << "  const int64_t o = (int64_t)(blockIdx.x >> 2) * bs;\n";
+            o << "  rbamd::dev::fdh_lane<T, N, " << F
+              << ">(kModel, q + o, qd + o, tau + o, qdd + o, ((blockIdx.x & 3u) << 6) + threadIdx.x, ld);\n}\n";
+        } else if (fdh && pack == 7) {
+            o << "  rbamd::dev::fdh_resident_lds<T, N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
+        } else if (fdh && pack == 5) {
             o << "  rbamd::dev::fdh_split_block1<T, N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
         } else if (fdh && pack == 4) {
             o << "  rbamd::dev::fdh_split_block2<N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
@@ -405,6 +420,13 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     // recursion into v_pk ops whose register pairs push the 30-link kernel to 256 VGPRs + 242
     // AGPRs (1 wave/SIMD); without it 243 VGPRs, 2 waves/SIMD like the one-chunk kernel.
     if (src.find("rnea_resident_lds") != std::string::npos) optv.push_back("-fno-slp-vectorize");
+    // The resident-grid FD (pack 7): machine LICM hoists the model constants' fp64
+    // materialisations out of the chunk loop, where they hold registers across all of it (FR3
+    // fp64: 161 VGPRs, 3 waves/SIMD, instead of the one-chunk kernel's 124).
+    if (src.find("fdh_resident_lds") != std::string::npos) {
+        optv.push_back("-mllvm");
+        optv.push_back("-disable-machine-licm");
+    }
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)optv.size(), optv.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
@@ -464,8 +486,9 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack,
         jk.function = nullptr;
         return jk;
     }
-    if (jk.pack == 6) {  // persistent grid: every block resident at once
-        jk.block = 64;
+    if (jk.pack == 8) jk.block = 64;
+    if (jk.pack == 6 || jk.pack == 7) {  // persistent grid: every block resident at once
+        jk.block = jk.pack == 6 ? 64 : 256;
         int per_cu = 0;
         if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jk.function, (int)jk.block, 0) != hipSuccess ||
             per_cu < 1)

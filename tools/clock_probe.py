@@ -203,6 +203,15 @@ def run(seconds, B, only):
                 "in_kernel_span_us": round(span * 1e6, 2),
                 "residency": round(float(life.sum() / (1024 * wps * span)), 3),
                 "waves": waves, "waves_per_simd_limit": wps}
+        # where the unoccupied slots are: resident fraction of the 1024 x wps wave slots over
+        # 20 equal bins of the in-kernel span, and when the last wave started / the first ended
+        t0, t1 = s[:, 2].min(), s[:, 3].max()
+        edges = np.linspace(t0, t1, 21)
+        lo_, hi_ = np.maximum(s[ok, 2][:, None], edges[None, :-1]), np.minimum(s[ok, 3][:, None], edges[None, 1:])
+        occ = np.clip(hi_ - lo_, 0, None).sum(0) / (1024 * wps * (edges[1] - edges[0]))
+        line.update({"occupancy_by_twentieth": [round(float(v), 3) for v in occ],
+                     "last_start_us": round(float(s[:, 2].max() - t0) / 100, 2),
+                     "first_end_us": round(float(s[:, 3].min() - t0) / 100, 2)})
         if pack == 4:  # per role: wave w % 4 in {0, 1} bias torques, {2, 3} mass matrix + solve
             role = np.arange(waves) % 4 >= 2
             t0 = s[:, 2].min()

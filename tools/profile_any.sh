@@ -1,6 +1,7 @@
 #!/bin/bash
 # profile_round.sh for any python workload (e.g. tools/ab_bench.py --kernel rollout): a kernel
-# trace (--kernel-trace --stats) and the four separate PMC passes of the same command.
+# trace (--kernel-trace --stats) and the five separate PMC passes of the same command (the fifth:
+# VALU FLOP counters, for roofline.valu).
 # usage (via gpurun): tools/profile_any.sh TAG script.py [args...]
 #   outputs under gpurun_out/TAG/{trace,pmc_fetch,pmc_write,pmc_sq,pmc_grbm} + TAG_*.log
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -18,4 +19,5 @@ tools/gpu_steps.sh \
   "${TAG}_pmc_fetch" 300 "cd /tmp && rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $B" \
   "${TAG}_pmc_write" 300 "cd /tmp && rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $B" \
   "${TAG}_pmc_sq" 300 "cd /tmp && rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $O/pmc_sq -o run --output-format csv -- $B" \
-  "${TAG}_pmc_grbm" 300 "cd /tmp && rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS -d $O/pmc_grbm -o run --output-format csv -- $B"
+  "${TAG}_pmc_grbm" 300 "cd /tmp && rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS -d $O/pmc_grbm -o run --output-format csv -- $B" \
+  "${TAG}_pmc_flops" 300 "cd /tmp && rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES -d $O/pmc_flops -o run --output-format csv -- $B"

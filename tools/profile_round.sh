@@ -14,7 +14,7 @@ TAG=${1:?usage: profile_round.sh TAG [bench args]}
 shift
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
-B="python3 $R/bench.py --no-cpu-baseline --no-secondary $*"
+B="python3 $R/bench.py --no-cpu-baseline --no-secondary --steps ${PROF_STEPS:-300} $*"
 export TMPDIR=/tmp
 tools/gpu_steps.sh \
   "${TAG}_trace" 300 "cd /tmp && rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- $B" \

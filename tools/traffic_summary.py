@@ -55,6 +55,9 @@ def main():
     B = int(workload.rsplit("_b", 1)[1])
     es = 4 if "_f32_" in workload else 8
     alg = (8 if workload.startswith("rnea_fd") else 4) * n * es * B
+    if workload.startswith("rollout_"):  # K steps: K tau rows read, q and qd read and written
+        K = int(workload.split("_K")[1].split("_")[0])
+        alg = (K + 4) * n * es * B
     kind = workload.split("_")[0]
     out = {"workload": workload, "kernel": f"{regex} (model-specialised {kind.upper()})",
            "algorithmic_bytes_per_launch": alg}
@@ -88,11 +91,15 @@ def main():
     if fl:
         # gfx950 FLOP counters (pass pmc_flops): FLOPs the kernel's VALU executed per launch
         out["valu_flops_per_launch"] = fl
-    out["method"] = ("rocprofv3 --pmc passes FETCH_SIZE / WRITE_SIZE / SQ_* / GRBM_* run separately on "
+    out["method"] = ("rocprofv3 --pmc passes FETCH_SIZE / WRITE_SIZE / SQ_* / GRBM_* / SQ_INSTS_VALU_FLOPS_* run separately on "
                      "`bench.py --no-cpu-baseline --no-secondary`, kernels matching " + regex +
                      ", mean over the profiled launches; bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), "
                      "gfx950 FETCH_SIZE halving calibrated as this script's docstring says")
-    with open(os.path.join("profiles", f"traffic_{workload}.json"), "w") as f:
+    # TRAFFIC_OUT: where traffic_<workload>.json goes (default profiles/; on the GPU box a
+    # directory under gpurun_out/, which is what comes back)
+    dest = os.environ.get("TRAFFIC_OUT", "profiles")
+    os.makedirs(dest, exist_ok=True)
+    with open(os.path.join(dest, f"traffic_{workload}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in out if k not in ("sq_counters_per_launch", "grbm_per_launch", "method")}))
 
