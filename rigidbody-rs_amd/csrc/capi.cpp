@@ -97,7 +97,7 @@ struct Multibody {
         const rbamd::JitKernel *jk = nullptr;
     };
     mutable std::map<std::pair<const void *, const rbamd::JitKernel *>, JitPub> jit_pub;
-    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][8][2] = {};
+    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][6][2] = {};
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
@@ -184,7 +184,7 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
     const bool fst = fast && !f64;
     std::atomic<const Multibody::JitPub *> *slot = nullptr;
-    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 8) {
+    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 6) {
         slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][tail > 0 ? 1 : 0];
         if (const Multibody::JitPub *p = slot->load(std::memory_order_acquire))
             if (p->gen.load(std::memory_order_acquire) == rbamd::tuning_generation()) return p->jk;
@@ -293,14 +293,9 @@ unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
         const unsigned P = (T - S) & ~1u;
         return P / 2u + (T - P);
     }
-    if (jk->pack == 6 || jk->pack == 7) {  // resident grid over 64-configuration chunks (pack 7: 4 waves per block)
-        const unsigned chunks = (unsigned)(((uint64_t)B + (jk->pack == 6 ? 63u : 255u)) / (jk->pack == 6 ? 64u : 256u));
-        const unsigned r = jk->resident > 0 ? jk->resident : 1u;
-        return chunks < r ? chunks : r;
-    }
     // pack 2 / 3: two configurations per lane; pack 5: the one-per-lane wave split, 128 per block
     // (pack 4, the packed split, covers 256 per block like one per lane)
-    const unsigned per_block = jk->pack == 8 ? 64u : jk->pack == 5 ? 128u : 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
+    const unsigned per_block = jk->pack == 5 ? 128u : 256u * ((jk->pack == 2 || jk->pack == 3) ? 2u : 1u);
     return (unsigned)(((uint64_t)B + per_block - 1) / per_block);
 }
 

@@ -338,108 +338,5 @@ __device__ __forceinline__ void fdh_split_block1(const T *mdl, const T *__restri
     }
 }
 
-// Resident grid with LDS-staged joint rows (jit pack 7: one configuration per lane, 256-thread
-// blocks, every block resident at once).  The one-launch-per-wave grid of the large-batch FD
-// leaves SIMDs idle twice (clock probe occupancy profile, profiles/r04/clock_probe.jsonl): a wave
-// slot that frees is refilled only when a whole 4-wave block fits, and the last round of waves
-// ends over one wave lifetime (~10 us at 4 waves/SIMD) while the SIMDs drain one by one.  Here
-// each wave walks the batch in 64-configuration chunks c, c + G, ... (G = resident waves), so
-// every SIMD keeps its 4 waves and the same share of chunks to the end; right after copying chunk
-// c's q, qd rows out of its LDS buffer, the wave starts the direct global->LDS loads
-// (global_load_lds, no VGPRs) of chunk c + G into the same buffer, so the next chunk's rows land
-// during chunk c's dynamics.  tau is loaded after the bias sweep as in fdh_lane; chunk c's qdd
-// stays in registers until the next chunk's loads are issued and goes out then.  Each 8-byte row
-// element comes as two dword loads (lanes 0-63 fetch dwords 0-63 and 64-127 of the wave's 512-B
-// row segment: coalesced, and landing in LDS in element order).  LDS: 2N rows x 64 lanes x s
-// bytes per wave (fp64 FR3: 7 KB, 28 KB per block + the 4 KB sincos table).  Lanes past B read
-// the last configuration and store nothing; every wave leaves the loop after its last chunk.
-template <typename T, int N, bool FAST>
-__device__ __forceinline__ void fdh_resident_lds(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
-                                                 const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
-                                                 int64_t ld, int64_t bs) {
-    constexpr uint32_t kDw = sizeof(T) / 4;  // dwords per element
-    __shared__ T buf[4][2 * N][64];
-    // wave-uniform in SGPRs: the chunk index, its block base and the loop control
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
-    const uint32_t nch = (B + 63u) / 64u;
-    const uint32_t G = gridDim.x * 4u;
-    // chunk ch lies in one 256-configuration block (uniform base (ch / 4) * bs)
-    auto lane_off = [&](uint32_t ch) -> uint32_t {
-        const uint32_t b = ch * 64u + l;
-        return ((b < B ? b : B - 1u) & 255u) * (uint32_t)sizeof(T);
-    };
-    auto stage = [&](uint32_t ch) {
-        const int64_t o = (int64_t)(ch >> 2) * bs;
-        // dword k * 64 + l of the wave's row segment: element (k * 64 + l) / kDw, clamped below B
-        uint32_t doff[kDw];
-#pragma unroll
-        for (uint32_t k = 0; k < kDw; ++k) {
-            const uint32_t d = k * 64u + l, e = ch * 64u + d / kDw;
-            doff[k] = ((e < B ? e : B - 1u) & 255u) * (uint32_t)sizeof(T) + (d % kDw) * 4u;
-        }
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const T *rows[2] = {q + o + j * ld, qd + o + j * ld};
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-#pragma unroll
-                for (uint32_t k = 0; k < kDw; ++k) {
-                    gptr<const char> src = (gptr<const char>)rows[r] + doff[k];
-                    __builtin_amdgcn_global_load_lds(
-                        (gptr<const void>)src,
-                        (__attribute__((address_space(3))) void *)((char *)&buf[w][2 * j + r][0] + k * 256u), 4, 0,
-                        (RB_NT & 1) != 0 ? 2 : 0);
-                }
-        }
-    };
-    auto store = [&](uint32_t ch, const T (&xv)[N]) {
-        if (ch * 64u + l < B) {
-            const int64_t o = (int64_t)(ch >> 2) * bs;
-            const uint32_t off = lane_off(ch);
-#pragma unroll
-            for (int j = 0; j < N; ++j) st_row(qdd + o, j * ld, off, xv[j]);
-        }
-    };
-    uint32_t c = blockIdx.x * 4u + w;
-    if (c >= nch) return;  // the launcher's grid covers at most ceil(nch / 4) blocks
-    stage(c);
-    T xv[N];
-    uint32_t prev = 0;
-    bool have_prev = false;
-    for (;;) {
-        // the compiler does not order LDS reads after a pending global_load_lds: wait for this
-        // chunk's rows (and the previous chunk's tau loads / stores) explicitly
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        T qv[N], qdv[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            qv[j] = buf[w][2 * j][l];
-            qdv[j] = buf[w][2 * j + 1][l];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the buffer is refilled
-        const uint32_t nxt = c + G;
-        if (nxt < nch) stage(nxt);
-        if (have_prev) store(prev, xv);
-        __builtin_amdgcn_sched_barrier(0);
-        const int64_t o = (int64_t)(c >> 2) * bs;
-        const uint32_t off = lane_off(c);
-        fdh_eval<T, N, FAST>(
-            mdl, qv, qdv,
-            [&](T (&tv)[N]) {
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    tv[j] = ld_row(tau + o, j * ld, off);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            },
-            [&](int j, T v) { xv[j] = v; });
-        prev = c;
-        have_prev = true;
-        if (nxt >= nch) break;
-        c = nxt;
-    }
-    store(prev, xv);
-}
-
 }  // namespace dev
 }  // namespace rbamd

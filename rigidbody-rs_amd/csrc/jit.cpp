@@ -80,19 +80,12 @@ int jit_pack(JitKind kind, bool f64, int n) {
     // fp64 RNEA of chains up to 8 links: 125 VGPRs, still 4 waves/SIMD; FR3 2^20 tiled
     // 42.0-42.8 us steady where the one-per-lane kernel alternates between ~40.7 and ~48.8 us
     // phases, mean 44.3-44.6).
-    // 6 = resident grid of one-wave blocks with the next chunk's inputs staged in LDS by direct
-    // global->LDS loads (rnea_body.hip.hpp rnea_resident_lds: fp32 RNEA of long chains).
-    // 7 = the mass-matrix forward dynamics on a resident grid of 4-wave blocks, each wave's
-    // next chunk of q, qd rows staged in LDS the same way (fdh_body.hip.hpp fdh_resident_lds).
     const int v = tuning().pack;
-    if (v == 6) return (kind == JitKind::Rnea && !f64) ? 6 : 1;
     if (kind == JitKind::Rollout) return ((v < 0 || v == 2 || v == 4) && !f64 && n <= 8) ? (v == 4 ? 4 : 2) : 1;
     if (kind != JitKind::Fd && kind != JitKind::Rnea) return 1;
     if (v == 3) return 3;
     if (v == 4) return (kind == JitKind::Fd && !f64) ? 4 : 1;  // split packed waves (fdh_split_block2)
     if (v == 5) return (kind == JitKind::Fd && !f64) ? 5 : 1;  // split waves, one per lane (fdh_split_block1)
-    if (v == 7) return kind == JitKind::Fd ? 7 : 1;  // resident grid, LDS-staged rows (fdh_resident_lds)
-    if (v == 8) return kind == JitKind::Fd ? 8 : 1;  // one per lane in one-wave blocks
     if (v >= 0) return (v >= 2 && !f64 && kind == JitKind::Fd) ? 2 : 1;
     if (kind == JitKind::Rnea) return (f64 && n <= 8) ? 3 : 1;
     return (!f64 && n <= 8) ? 2 : 1;
@@ -127,9 +120,6 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
         return (!f64 && m.n <= 8) ? 2 : 1;  // the split needs the mass-matrix form: the pair instead
     if ((pack == 4 || pack == 5) && kind != JitKind::Rollout && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2))
         return 1;
-    if (pack == 6 && !(kind == JitKind::Rnea && !f64 && m.serial_revolute())) return 1;
-    // 7 = the resident-grid mass-matrix FD with LDS-staged rows (one configuration per lane)
-    if ((pack == 7 || pack == 8) && !(kind == JitKind::Fd && jit_fd_form(m) == 2)) return 1;
     return pack;
 }
 
@@ -285,12 +275,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     const char *head = head_s.c_str();
     // Lane kernels take the block stride bs (elements): 256 for SoA, N * 256 for the tiled
     // layout (kernels.hpp); block k's arrays start at element k * bs, lane offset threadIdx.x.
-    if (kind == JitKind::Rnea && pack == 6) {
-        o << "extern \"C\" __global__ __launch_bounds__(64) void rb_jit_kernel(const T *__restrict__ q, "
-             "const T *__restrict__ qd, const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, "
-             "int64_t bs) {\n";
-        o << "  rbamd::dev::rnea_resident_lds<T, N, " << F << ">(kModel, q, qd, qdd, tau, B, ld, bs);\n}\n";
-    } else if (kind == JitKind::Rnea && pack == 3 && tail > 0) {
+    if (kind == JitKind::Rnea && pack == 3 && tail > 0) {
         // pairs of tiles for blocks < G1, then one tile per block for the last S tiles
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
@@ -320,18 +305,9 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
         o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n}\n";
     } else if (kind == JitKind::Fd) {
-        // pack 8: one-wave blocks, so a wave slot that frees is refilled by the next wave alone
-        o << (fdh && pack == 8 ? head_s.replace(head_s.find("(256)"), 5, "(64)").c_str() : head) << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+        o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";
-        if (fdh && pack == 8) {
-            o << "  const uint32_t b = blockIdx.x * 64u + threadIdx.x;\n";
-            o << "  if (b >= B) return;\n";
-            o << "  const int64_t o = (int64_t)(blockIdx.x >> 2) * bs;\n";
-            o << "  rbamd::dev::fdh_lane<T, N, " << F
-              << ">(kModel, q + o, qd + o, tau + o, qdd + o, ((blockIdx.x & 3u) << 6) + threadIdx.x, ld);\n}\n";
-        } else if (fdh && pack == 7) {
-            o << "  rbamd::dev::fdh_resident_lds<T, N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
-        } else if (fdh && pack == 5) {
+        if (fdh && pack == 5) {
             o << "  rbamd::dev::fdh_split_block1<T, N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
         } else if (fdh && pack == 4) {
             o << "  rbamd::dev::fdh_split_block2<N, " << F << ">(kModel, q, qd, tau, qdd, B, ld, bs);\n}\n";
@@ -416,17 +392,6 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
         optv.push_back("-mllvm");
         optv.push_back("-disable-machine-licm");
     }
-    // The resident-grid RNEA (pack 6): inside its chunk loop the SLP vectorizer pairs the fp32
-    // recursion into v_pk ops whose register pairs push the 30-link kernel to 256 VGPRs + 242
-    // AGPRs (1 wave/SIMD); without it 243 VGPRs, 2 waves/SIMD like the one-chunk kernel.
-    if (src.find("rnea_resident_lds") != std::string::npos) optv.push_back("-fno-slp-vectorize");
-    // The resident-grid FD (pack 7): machine LICM hoists the model constants' fp64
-    // materialisations out of the chunk loop, where they hold registers across all of it (FR3
-    // fp64: 161 VGPRs, 3 waves/SIMD, instead of the one-chunk kernel's 124).
-    if (src.find("fdh_resident_lds") != std::string::npos) {
-        optv.push_back("-mllvm");
-        optv.push_back("-disable-machine-licm");
-    }
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)optv.size(), optv.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
@@ -485,15 +450,6 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack,
         jk.module = nullptr;
         jk.function = nullptr;
         return jk;
-    }
-    if (jk.pack == 8) jk.block = 64;
-    if (jk.pack == 6 || jk.pack == 7) {  // persistent grid: every block resident at once
-        jk.block = jk.pack == 6 ? 64 : 256;
-        int per_cu = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jk.function, (int)jk.block, 0) != hipSuccess ||
-            per_cu < 1)
-            per_cu = 1;
-        jk.resident = (unsigned)per_cu * (unsigned)(prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256);
     }
     return jk;
 }

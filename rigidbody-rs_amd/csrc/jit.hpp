@@ -32,8 +32,7 @@ struct JitKernel {
     hipFunction_t function = nullptr;  // the lane kernel (any layout)
     int pack = 1;                      // configurations per lane (2: paired fp32 lanes, 512 per block)
     int seq_tail = 0;                  // pack 3: trailing tiles run one per lane (tuning seq_tail)
-    unsigned block = 256;              // threads per block (pack 6: one-wave blocks)
-    unsigned resident = 0;             // pack 6: blocks resident on the device (the persistent grid)
+    unsigned block = 256;              // threads per block
     std::string error;                 // non-empty when compilation failed
 };
 

@@ -187,86 +187,6 @@ __device__ __forceinline__ void rnea_lane_seq2(const T *mdl, const T *__restrict
     if (two) rnea_any<T, N, FAST, Topo>(mdl, qb, qdb, qddb, [&](int j, T v) { st_row(tau, j * ld, offB, v); });
 }
 
-// Resident grid with LDS-staged inputs (jit pack 6: fp32 one configuration per lane, long
-// chains).  The 30-link chain's lane holds ~240 live values at the end of its forward sweep
-// (246 VGPRs), so only 2 waves fit a SIMD; with every wave loading, then computing, then
-// storing, the two waves of a SIMD run in step and the memory pipe idles while they compute
-// (100 us against an 81 us no-math probe of the same access pattern).  Here each
-// one-wave block walks the batch in 64-configuration chunks c, c + G, ... (G = resident blocks)
-// and, right after copying chunk c's inputs out of its LDS buffer into registers, starts the
-// direct global->LDS loads (global_load_lds, no VGPRs) of chunk c + G into the same buffer, so
-// the next chunk's 90 rows are in flight during the whole of chunk c's dynamics.  Chunk c's
-// torques stay in registers until after that issue (the stores then drain under the compute)
-// and go out at the top of the next round.  LDS: 3N rows x 64 lanes x 4 B per wave (23 KB at
-// N = 30, 6 waves per CU).  Lanes past B read the last configuration and store nothing.
-template <typename T, int N, bool FAST>
-__device__ __forceinline__ void rnea_resident_lds(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
-                                                  const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B,
-                                                  int64_t ld, int64_t bs) {
-    static_assert(sizeof(T) == 4, "one dword per lane per row");
-    __shared__ T buf[3 * N][64];
-    const uint32_t l = threadIdx.x;  // one-wave blocks
-    const uint32_t nch = (B + 63u) / 64u;
-    // chunk ch lies in one 256-configuration block (uniform base ch / 4 * bs); lanes past B
-    // read the last configuration, which is in the same block
-    auto lane_off = [&](uint32_t ch) -> uint32_t {
-        const uint32_t b = ch * 64u + l;
-        return ((b < B ? b : B - 1u) & 255u) * (uint32_t)sizeof(T);
-    };
-    auto stage = [&](uint32_t ch) {
-        const int64_t o = (int64_t)(ch >> 2) * bs;
-        const uint32_t off = lane_off(ch);
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const T *rows[3] = {q + o + j * ld, qd + o + j * ld, qdd + o + j * ld};
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                // saddr form: uniform row base + the lane's 32-bit byte offset (spatial.hip.hpp ld_row)
-                gptr<const char> src = (gptr<const char>)rows[k] + off;
-                __builtin_amdgcn_global_load_lds((gptr<const void>)src,
-                                                 (__attribute__((address_space(3))) void *)&buf[3 * j + k][0], 4, 0,
-                                                 (RB_NT & 1) != 0 ? 2 : 0);
-            }
-        }
-    };
-    auto store = [&](uint32_t ch, const T (&tv)[N]) {
-        if (ch * 64u + l < B) {
-            const int64_t o = (int64_t)(ch >> 2) * bs;
-            const uint32_t off = lane_off(ch);
-#pragma unroll
-            for (int j = 0; j < N; ++j) st_row(tau + o, j * ld, off, tv[j]);
-        }
-    };
-    uint32_t c = blockIdx.x;  // the launcher's grid never exceeds nch
-    stage(c);
-    T tv[N];
-    uint32_t prev = 0;
-    bool have_prev = false;
-    for (;;) {
-        // the compiler does not order LDS reads after a pending global_load_lds: wait for this
-        // chunk's staging (and the previous round's stores, long retired) explicitly
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        T qv[N], qdv[N], qddv[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            qv[j] = buf[3 * j][l];
-            qdv[j] = buf[3 * j + 1][l];
-            qddv[j] = buf[3 * j + 2][l];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the buffer is refilled
-        const uint32_t nxt = c + gridDim.x;
-        if (nxt < nch) stage(nxt);
-        if (have_prev) store(prev, tv);
-        __builtin_amdgcn_sched_barrier(0);
-        rnea_eval<T, N, FAST>(mdl, qv, qdv, qddv, [&](int j, T v) { tv[j] = v; });
-        prev = c;
-        have_prev = true;
-        if (nxt >= nch) break;
-        c = nxt;
-    }
-    store(prev, tv);
-}
-
 // Streaming form (precompiled generic kernels, rnea.hip): walk the batch with `stride`,
 // prefetching the next configuration's joint values into registers before evaluating the
 // current one.

@@ -458,10 +458,10 @@ struct alignas(16) SinCosEntry {
 __shared__ SinCosEntry rb_sctab[256];
 
 // Every wave of the block must call this before any sin_cos(double) (it ends in a barrier);
-// 256-thread blocks copy one entry per thread, 64-thread blocks four.
+// blocks are 256 threads, one entry each.
 __device__ __forceinline__ void sctab_init() {
-    for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x)
-        rb_sctab[t] = SinCosEntry{rb_sctab_src[2 * t], rb_sctab_src[2 * t + 1]};
+    const uint32_t t = threadIdx.x;
+    rb_sctab[t] = SinCosEntry{rb_sctab_src[2 * t], rb_sctab_src[2 * t + 1]};
     __syncthreads();
 }
 

@@ -281,92 +281,6 @@ def test_chain30_full_size_f32(ffi, dev):
           f"affine {worst_aff:.2e}, fd32 backward K {K:.1f}")
 
 
-@pytest.mark.parametrize("model", ["chain30", "fr3"])
-def test_resident_lds_rnea_bit_identical(model, ffi, dev, fr3_text):
-    """The resident-grid RNEA with LDS-staged inputs (jit pack 6, rnea_body.hip.hpp
-    rnea_resident_lds: one-wave blocks walking 64-configuration chunks, the next chunk's rows
-    loaded straight into LDS during the current one's dynamics) is the same per-lane
-    arithmetic as the one-per-lane kernel: bit-identical on ragged batches (a partial last
-    chunk, batches larger and smaller than the resident grid), SoA with ld > B (padding
-    untouched) and tiled; oracle spot columns (multibody.rs:111-153, fp32 1e-4)."""
-    from rigidbody_amd import chains
-
-    xml = chains.synthetic_chain_urdf(30) if model == "chain30" else fr3_text
-    mb = ffi.Multibody.from_urdf_string(xml)
-    om = _oracle(xml)
-    n, lim = mb.n, mb.limits()
-    for B in (1, 63, 65, 1000, 300007):
-        ld = B + 5
-        full = [torch.full((n, ld), 7.0, dtype=torch.float32, device=dev) for _ in range(3)]
-        for k, kind in enumerate(("q", "qd", "qdd")):
-            full[k][:, :B] = _t(chains.host_uniform(n, B, *chains.input_ranges(lim, kind), chains.SEED + 90 + k,
-                                                    dtype="float32"), dev, torch.float32)
-        x = [f[:, :B] for f in full]
-        res = {}
-        try:
-            for pack in (1, 6):
-                ffi.set_tuning("pack", pack)
-                assert mb.kernel_form("rnea", False, B) == pack
-                out = torch.full((n, ld), 123.0, dtype=torch.float32, device=dev)
-                mb.rnea_batch(*x, out=out[:, :B])
-                assert torch.all(out[:, B:] == 123.0), (B, pack)
-                til = ffi.from_tiled(mb.rnea_batch_tiled(*[ffi.to_tiled(a.contiguous()) for a in x], B), B)
-                res[pack] = (out[:, :B].cpu().numpy(), til.cpu().numpy())
-        finally:
-            ffi.set_tuning("pack", -1)
-        np.testing.assert_array_equal(res[6][0], res[1][0], err_msg=f"{model} B={B} soa")
-        np.testing.assert_array_equal(res[6][1], res[1][1], err_msg=f"{model} B={B} tiled")
-        np.testing.assert_array_equal(res[6][0], res[6][1], err_msg=f"{model} B={B} soa vs tiled")
-        idx = np.unique(np.linspace(0, B - 1, min(B, 256)).astype(int))
-        xs = [a[:, idx].double().cpu().numpy() for a in x]
-        ref = om.rnea_batch(*xs)
-        got = res[6][0][:, idx].astype(np.float64)
-        assert (np.abs(got - ref).max(0) / (1 + np.abs(ref).max(0))).max() <= 1e-4, (model, B)
-
-
-def test_fd_grid_forms_bit_identical(ffi, dev, fr3_text):
-    """Two grid forms of the fp64 mass-matrix forward dynamics run the per-lane arithmetic of the
-    one-per-lane kernel (jit pack 1) and must match it bit for bit:
-    - pack 7, fdh_body.hip.hpp fdh_resident_lds: a resident grid of 4-wave blocks walking
-      64-configuration chunks, the next chunk's q, qd rows loaded straight into LDS (two dword
-      loads per fp64 element) during the current chunk's dynamics;
-    - pack 8: the one-per-lane kernel in one-wave blocks (the sincos table copied per wave).
-    Ragged batches (a partial last chunk; grids below and above the resident size: 2^20 + 77 is
-    ~4 chunks per wave), SoA with ld > B (padding untouched) and tiled; torque residual against
-    the oracle on spot columns (the A10 definition, multibody.rs:111-174)."""
-    from rigidbody_amd import chains
-
-    mb = ffi.Multibody.from_urdf_string(fr3_text)
-    om = _oracle(fr3_text)
-    n, lim = mb.n, mb.limits()
-    for B in (1, 63, 65, 1000, 300007, (1 << 20) + 77):
-        ld = B + 5
-        full = [torch.full((n, ld), 7.0, dtype=torch.float64, device=dev) for _ in range(3)]
-        for k, kind in enumerate(("q", "qd", "tau")):
-            full[k][:, :B] = _t(chains.host_uniform(n, B, *chains.input_ranges(lim, kind), chains.SEED + 95 + k), dev)
-        x = [f[:, :B] for f in full]
-        res = {}
-        try:
-            for pack in (1, 7, 8):
-                ffi.set_tuning("pack", pack)
-                assert mb.kernel_form("fd", True, B) == pack
-                out = torch.full((n, ld), 123.0, dtype=torch.float64, device=dev)
-                mb.fd_batch(*x, out=out[:, :B])
-                assert torch.all(out[:, B:] == 123.0), (B, pack)
-                til = ffi.from_tiled(mb.fd_batch_tiled(*[ffi.to_tiled(a.contiguous()) for a in x], B), B)
-                res[pack] = (out[:, :B].cpu().numpy(), til.cpu().numpy())
-        finally:
-            ffi.set_tuning("pack", -1)
-        for pack in (7, 8):
-            np.testing.assert_array_equal(res[pack][0], res[1][0], err_msg=f"pack {pack} B={B} soa")
-            np.testing.assert_array_equal(res[pack][1], res[1][1], err_msg=f"pack {pack} B={B} tiled")
-        np.testing.assert_array_equal(res[1][0], res[1][1], err_msg=f"B={B} soa vs tiled")
-        idx = np.unique(np.linspace(0, B - 1, min(B, 256)).astype(int))
-        xs = [a[:, idx].cpu().numpy() for a in x]
-        r = np.abs(om.rnea_batch(xs[0], xs[1], res[1][0][:, idx]) - xs[2]) / (1 + np.abs(xs[2]))
-        assert r.max() <= 1e-8, (B, r.max())
-
-
 def test_full_size_properties(ffi, dev, fr3_text):
     """BASELINE config size (fr3, B = 2^20): the oracle cannot cover every column, so
     check size-independent properties on all of them plus an oracle spot check:

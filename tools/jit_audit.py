@@ -30,10 +30,6 @@ def main():
            "-Rpass-analysis=kernel-resource-usage", path]
     if kind == "rollout" and "RB_ROLLOUT_NO_HOIST 1" in src:  # as jit.cpp compiles it
         cmd[1:1] = ["-mllvm", "-disable-machine-licm"]
-    if "fdh_resident_lds" in src:
-        cmd[1:1] = ["-mllvm", "-disable-machine-licm"]
-    if "rnea_resident_lds" in src:
-        cmd[1:1] = ["-fno-slp-vectorize"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:
         print(r.stderr[-4000:])
