@@ -455,9 +455,10 @@ def side_workloads(mb7, a):
         if kernel in ("rnea", "fd"):
             model = "fr3" if mb.n == 7 else f"chain{mb.n}" if "tree" not in name else None
             if model:
+                form = mb.kernel_form(kernel, dt_name == "f64", B, layout == "tiled")
                 sec[name]["valu"] = valu_roofline(workload_name(kernel, mb.n, dt_name, layout, B), f"{kernel}_{model}",
                                                   f"{kernel}_{model}_{dt_name}" + ("" if B == a.batch else f"_b{B}"),
-                                                  dt_name, B, r["kernel_ms_avg"])
+                                                  dt_name, B, r["kernel_ms_avg"], form in (2, 4))
         if graph:  # the same launches replayed from a HIP graph; rates over the launches replayed
             gl = r["graph_launches"]
             # eager back-to-back launches from Python are host-bound when the graph replay of the
@@ -501,7 +502,7 @@ def side_workloads(mb7, a):
                                         "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", dn == "f64"),
                                         "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)",
                                         "valu": valu_roofline(f"rollout_fr3_{dn}_K16_b{a.batch}", "rollout_step_fr3",
-                                                              f"rollout_fr3_{dn}", dn, a.batch * K, km)}
+                                                              f"rollout_fr3_{dn}", dn, a.batch * K, km, dn == "f32")}
     # the MPC-sized rollout (65536 configurations, K = 16): the split of packed waves per step
     # (rollout_split_block2), device-bound rate from a HIP graph
     Bs = 65536
@@ -648,28 +649,38 @@ def held_clock(name):
     return None
 
 
-def valu_roofline(workload, op_key, clock_key, dt_name, evals, kern_ms):
+def valu_roofline(workload, op_key, clock_key, dt_name, evals, kern_ms, packed):
     """roofline.valu for a VALU-heavy kernel (SURVEY §8(d) "reported alongside"): the committed
     PMC counters of this workload's kernel (profiles/traffic_<workload>.json) over this run's
-    kernel time.  issue_frac = SIMD cycles of VALU issue (SQ_ACTIVE_INST_VALU, quad-cycles x 4,
-    summed over waves) / (1024 SIMDs x clock x kernel time), at 2.4 GHz and at the clock the chip
-    holds under this kernel (clock probe); flop_frac = VALU FLOPs executed (gfx950
-    SQ_INSTS_VALU_FLOPS_*) / the dtype's vector peak; flops_per_eval_ref = the reference
-    formulation's operations per evaluation (op-counting oracle build, profiles/r04/op_counts.json)."""
+    kernel time.
+      issue_frac = SQ_INSTS_VALU x cycles per wave64 VALU instruction / (1024 SIMDs x clock x
+        kernel time): the fraction of the SIMDs' vector issue the kernel's instructions fill, at
+        2.4 GHz and at the clock the chip holds under this kernel (clock probe).  4 cycles for
+        fp64 and packed fp32 (v_pk_*) kernels (the measured wave64 issue of v_fma_f64 /
+        v_pk_fma_f32: 16 lanes/clk/SIMD fp64, 2 x 16 packed), 2 for scalar fp32 (32 lanes/clk,
+        MI355X_MICROARCH.md 'Per-instruction cycle constants').
+      flop_frac = VALU FLOPs executed (gfx950 SQ_INSTS_VALU_FLOPS_*, x 64 lanes) / the dtype's
+        vector peak (fp32 157.3 TF, fp64 78.6 TF at 2.4 GHz).
+      flops_per_eval_ref = the reference formulation's operations per evaluation (op-counting
+        oracle build, profiles/r04/op_counts.json) -- what the kernel replaces, not what it runs."""
     tr = load_traffic(workload)
     ops = _load_json("profiles/r04/op_counts.json")
     t = kern_ms * 1e-3
-    out = {"bound": "valu", "unit": "fraction", "evals_per_launch": evals}
+    cyc = 4 if (dt_name == "f64" or packed) else 2
+    out = {"bound": "valu", "unit": "fraction", "evals_per_launch": evals, "cycles_per_valu_inst": cyc}
     if ops and op_key in ops:
         ref = ops[op_key]["flops"]
         out.update({"flops_per_eval_ref": ref, "ref_equiv_tflops": ref * evals / t / 1e12,
                     "ref_source": f"profiles/r04/op_counts.json [{op_key}] (oracle/flops.cpp)"})
     sq = (tr or {}).get("sq_counters_per_launch", {})
-    if "SQ_INSTS_VALU" in sq and "SQ_ACTIVE_INST_VALU" in sq:
-        busy = sq["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS  # VALU issue cycles per SIMD per launch
-        out.update({"insts_per_eval": sq["SQ_INSTS_VALU"] / evals,
-                    "issue_cycles_per_eval": sq["SQ_ACTIVE_INST_VALU"] * 4 / evals,
+    if "SQ_INSTS_VALU" in sq:
+        busy = sq["SQ_INSTS_VALU"] * cyc / SIMDS  # vector issue cycles per SIMD per launch
+        # SQ_INSTS_VALU counts wave-instructions: x 64 lanes / evaluations = the VALU instructions
+        # one lane issues per configuration it evaluates (half a packed pair's stream)
+        out.update({"insts_per_eval": sq["SQ_INSTS_VALU"] * 64 / evals,
                     "issue_frac_2p4ghz": busy / (CLOCK_PEAK * t)})
+        if "SQ_ACTIVE_INST_VALU" in sq:  # wave-cycles a VALU instruction holds its wave (quad-cycles x 4)
+            out["wave_cycles_per_valu_inst"] = sq["SQ_ACTIVE_INST_VALU"] * 4 / sq["SQ_INSTS_VALU"]
         clk = held_clock(clock_key)
         if clk:
             out.update({"held_clock_ghz": clk, "issue_frac_held": busy / (clk * 1e9 * t),
@@ -754,8 +765,9 @@ def main(a):
         line["roofline"]["traffic_source"] = f"profiles/traffic_{workload}.json (rocprofv3 PMC passes)"
     if not a.stub:
         model = "fr3" if n == 7 else f"chain{n}"
+        form = mb.kernel_form(a.kernel.split("_")[0], a.dtype == "f64", B, a.layout == "tiled")
         line["roofline"]["valu"] = valu_roofline(workload, f"{a.kernel.split('_')[0]}_{model}",
-                                                 f"{a.kernel}_{model}_{a.dtype}", a.dtype, B, kern_ms)
+                                                 f"{a.kernel}_{model}_{a.dtype}", a.dtype, B, kern_ms, form in (2, 4))
     if world > 1:
         line["per_rank"] = ranks
     sec = {}

@@ -112,3 +112,25 @@ def test_batch_launcher_owns_its_sets():
     del launch
     gc.collect()
     assert ref() is None
+
+
+@pytest.mark.parametrize("workload,op,clock,dt,packed,ms", [
+    ("fd_fr3_f64_tiled_b1048576", "fd_fr3", "fd_fr3_f64", "f64", False, 0.051),
+    ("fd_fr3_f32_tiled_b1048576", "fd_fr3", "fd_fr3_f32", "f32", True, 0.0256),
+    ("rnea_chain30_f32_tiled_b1048576", "rnea_chain30", "rnea_chain30_f32", "f32", False, 0.1019),
+])
+def test_valu_roofline_from_committed_counters(workload, op, clock, dt, packed, ms):
+    """roofline.valu from the committed PMC summary (profiles/traffic_*.json), the op-counting
+    oracle's FLOPs (profiles/r04/op_counts.json) and the clock probe (profiles/r04/
+    clock_probe.jsonl) at a kernel time of the measured order: every fraction present and in
+    (0, 1], the FLOP counters scaled to lanes (kernel FLOPs per evaluation within 2x of the
+    VALU instruction count per evaluation x 2 per FMA)."""
+    sys.path.insert(0, REPO)
+    sys.argv = ["bench.py"]
+    bench = pytest.importorskip("bench")
+    v = bench.valu_roofline(workload, op, clock, dt, 1 << 20, ms, packed)
+    for k in ("issue_frac_2p4ghz", "issue_frac_held", "flop_frac"):
+        assert 0 < v[k] <= 1.0, (k, v[k])
+    assert v["held_clock_ghz"] < 2.4 and v["flops_per_eval_ref"] > 1000
+    per_inst = v["kernel_flops_per_eval"] / v["insts_per_eval"]
+    assert 0.5 < per_inst < (4.5 if packed else 2.5), per_inst
