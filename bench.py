@@ -540,6 +540,25 @@ def single_call(iters=2000):
     return out
 
 
+def native_batch(cases=(("rnea", "f32", 65536), ("fd", "f32", 65536), ("rnea", "f64", 131072), ("fd", "f64", 131072))):
+    """SURVEY §8(d) configs 2 / 3 (and config 4's 2^17 fp64 shard) as a native caller drives the
+    batched C ABI: examples/batch_bench.cpp, a child process linked against
+    librigidbody_bindings.so -- eager back-to-back calls on one stream (and their host cost per
+    call) and the same calls replayed from a HIP graph, tiled layout, no Python in the loop."""
+    exe = os.path.join(REPO, "rigidbody-rs_amd", "bin", "batch_bench")
+    if not os.path.exists(exe):
+        return {"error": f"{exe} not built (make -C rigidbody-rs_amd)"}
+    out = {}
+    for kind, dt, B in cases:
+        r = subprocess.run([exe, kind, dt, str(B), "20000", "tiled"], capture_output=True, text=True, timeout=300)
+        key = f"{kind}_fr3_{dt}_b{B}"
+        out[key] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {"error": r.stderr[-500:]}
+    out["how"] = ("C++ consumer (examples/batch_bench.cpp): 20000 calls of multibody_{rnea,fd}_batch_tiled_* over "
+                  "input sets rotated through >= 1.25 GiB, hipEvent pair on the stream; eager = back-to-back calls, "
+                  "graph = the same calls captured 100 per HIP graph and replayed")
+    return out
+
+
 def host_cores():
     try:
         return len(os.sched_getaffinity(0))
@@ -804,6 +823,7 @@ def main(a):
             sec[f"layout_ab_{kern}_{dt_name}"] = layout_ab(mb, kern, dt_name, a.batch)
         sec.update(side_workloads(mb, a))
         sec["single_call"] = single_call()
+        sec["native_batch"] = native_batch()
         if "cpu_baseline" in line:
             cb = line["cpu_baseline"]
             sec["single_call"]["oracle_single_thread_us"] = {"rnea": cb["single_thread_us_per_call"],
