@@ -395,6 +395,29 @@ def test_cpp_consumer_drop_in(tmp_path, dev):
     _close(lines["crba"], g["crba_raw"], 1e-9, "consumer crba")
 
 
+def test_cpp_batch_consumer(dev):
+    """examples/batch_bench.cpp, the prebuilt native caller of the batched device-pointer ABI
+    (rigidbody-rs_amd/bin/batch_bench, bench.py secondary.native_batch): runs as its own process
+    on ragged and config-size batches, both dtypes and layouts, and reports the kernel form the
+    launch policy takes (multibody_kernel_form_ex) with positive eager / graph times."""
+    import json
+    import os
+    import subprocess
+
+    from conftest import PKG
+
+    exe = os.path.join(PKG, "bin", "batch_bench")
+    assert os.path.exists(exe), "make -C rigidbody-rs_amd bin/batch_bench"
+    for kind, dt, B, layout, form in (("rnea", "f32", 65536, "tiled", 1), ("fd", "f32", 65536, "tiled", 4),
+                                      ("fd", "f64", 1000, "soa", 1), ("rnea", "f64", 300007, "tiled", 1)):
+        r = subprocess.run([exe, kind, dt, str(B), "200", layout], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert (d["kind"], d["dtype"], d["batch"], d["layout"]) == (kind, dt, B, layout)
+        assert d["kernel_form"] == form, d
+        assert d["eager_us_per_call"] > 0 and d["graph_us_per_call"] > 0 and d["host_us_per_call"] > 0
+
+
 
 def test_small_batch_fd_forms_strided(ffi, dev, fr3_text):
     """The small-batch forward-dynamics forms (policy: the one-per-lane wave split, pack 5, up to
