@@ -347,6 +347,38 @@ def batch_launcher(mb, sets, kernel, dtype, layout="soa", B=None):
     return launch
 
 
+# the batched mass matrix and kinematics read q (n rows) and write
+# rows_out rows per configuration (SoA, one write each): CRBA n*n (the ABI's column-major matrix,
+# lower triangle exact zeros), Jacobian 6n, forward kinematics 3
+Q_KERNELS = {"crba": lambda n: n * n, "jac": lambda n: 6 * n, "fwd_kin": lambda n: 3}
+
+
+def q_launcher(mb, kernel, B, dtype, rotate_gib, seed=chains.SEED):
+    """Closure issuing multibody_{crba,jac,fwd_kin}_batch_* on input set i % nsets (q only);
+    returns (launch, bytes per launch)."""
+    n, rows = mb.n, Q_KERNELS[kernel](mb.n)
+    es = 4 if dtype == torch.float32 else 8
+    per = (n + rows) * B * es
+    ns = max(2, int(np.ceil(rotate_gib * (1 << 30) / per)))
+    lo, hi = chains.input_ranges(mb.limits(), "q")
+    qs, outs = [], []
+    for s in range(ns):
+        q = torch.empty((n, B), dtype=dtype, device="cuda")
+        ffi.fill_uniform(q, lo, hi, seed + 1000 * s)
+        qs.append(q)
+        outs.append(torch.empty((rows, B), dtype=dtype, device="cuda"))
+    torch.cuda.synchronize()
+    fn = getattr(ffi.lib(), f"multibody_{kernel}_batch_{'f32' if dtype == torch.float32 else 'f64'}")
+    calls = [(mb.handle, q.data_ptr(), o.data_ptr(), B, B) for q, o in zip(qs, outs)]
+
+    def launch(i, sp):
+        if fn(*calls[i % ns], sp):
+            raise RuntimeError(ffi.last_error())
+
+    launch.keep = (qs, outs)
+    return launch, per
+
+
 def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED):
     """Closure issuing multibody_rollout_batch_* on one resident state (q, qd updated in
     place by every launch) and a [K*n, B] torque sequence."""
@@ -491,6 +523,20 @@ def side_workloads(mb7, a):
     mbt.upload()
     one("rnea_float14_tree_f32", mbt, "rnea", "f32")
     one("fd_float14_tree_f32", mbt, "fd", "f32")
+    # batched mass matrix / Jacobian / forward kinematics: q in, n*n /
+    # 6n / 3 rows out per configuration, SoA, 2^20 configurations
+    for kern in ("crba", "jac", "fwd_kin"):
+        for dn, dt in (("f64", torch.float64), ("f32", torch.float32)):
+            ql, per = q_launcher(mb7, kern, a.batch, dt, a.rotate_gib)
+            nl = budget_steps(ql)
+            w, km = time_launches(ql, nl, 3, 1, 100.0)
+            sec[f"{kern}_fr3_{dn}"] = {"evals_per_s": a.batch * nl / w, "kernel_ms_avg": km, "batch": a.batch,
+                                       "launches": nl, "layout": "soa", "dtype": dn,
+                                       "bytes_per_eval": per // a.batch,
+                                       "hbm_frac": per / (km * 1e-3) / HBM_PEAK,
+                                       "kernel_path": mb7.kernel_path(kern, dn == "f64", a.batch)}
+            del ql
+    torch.cuda.empty_cache()
     # fused rollout: K forward-dynamics + Euler steps per launch
     K = 16
     for dn, dt in (("f32", torch.float32), ("f64", torch.float64)):

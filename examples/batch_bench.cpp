@@ -7,7 +7,9 @@
 // Three timings of the same K calls (hipEvent pair on the launch stream, after warm-up):
 //   eager   K back-to-back calls of the C entry point on one stream (host cost included when it
 //           exceeds the device time: the launch-bound rate a caller gets without graphs)
-//   host    the host time per call of that loop (std::chrono; the C ABI + hipModuleLaunchKernel)
+//   host    the host time per call of that loop (std::chrono; the C ABI + hipModuleLaunchKernel),
+//           beside the host time per launch of an empty kernel of the same grid (the runtime's
+//           own floor)
 //   graph   the same calls captured once into a HIP graph (100 per graph) and replayed
 //
 // usage: batch_bench KIND DTYPE B [K] [tiled]   KIND rnea|fd, DTYPE f32|f64
@@ -24,6 +26,12 @@
 #include <vector>
 
 #include "rigidbody_batch.h"
+
+// An empty kernel: the HIP runtime's own launch cost, against which the C ABI's host cost per
+// call is read.
+__global__ void empty_kernel(int *p) {
+    if (p && threadIdx.x == 1024) *p = 0;
+}
 
 namespace {
 
@@ -126,6 +134,15 @@ int run(const char *kind, int64_t B, int K, bool tiled) {
     float eager_ms = 0;
     CHECK_HIP(hipEventElapsedTime(&eager_ms, e0, e1));
     const double host_us = std::chrono::duration<double, std::micro>(h1 - h0).count() / K;
+    // the runtime's floor: K launches of an empty kernel of the same grid from this thread
+    const unsigned grid = (unsigned)((B + 255) / 256);
+    for (int i = 0; i < 100; ++i) hipLaunchKernelGGL(empty_kernel, dim3(grid), dim3(256), 0, st, nullptr);
+    CHECK_HIP(hipStreamSynchronize(st));
+    auto g0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < K; ++i) hipLaunchKernelGGL(empty_kernel, dim3(grid), dim3(256), 0, st, nullptr);
+    auto g1 = std::chrono::steady_clock::now();
+    CHECK_HIP(hipStreamSynchronize(st));
+    const double empty_host_us = std::chrono::duration<double, std::micro>(g1 - g0).count() / K;
     // graph: 100 consecutive calls captured once, replayed
     const int per = 100, reps = std::max(1, K / per);
     hipGraph_t g;
@@ -144,11 +161,12 @@ int run(const char *kind, int64_t B, int K, bool tiled) {
     CHECK_HIP(hipEventElapsedTime(&graph_ms, e0, e1));
     const double eager_us = eager_ms * 1e3 / K, graph_us = graph_ms * 1e3 / (reps * per);
     std::printf("{\"kind\": \"%s\", \"dtype\": \"%s\", \"batch\": %lld, \"layout\": \"%s\", \"calls\": %d, "
-                "\"eager_us_per_call\": %.3f, \"host_us_per_call\": %.3f, \"graph_us_per_call\": %.3f, "
+                "\"eager_us_per_call\": %.3f, \"host_us_per_call\": %.3f, \"empty_kernel_host_us\": %.3f, "
+                "\"graph_us_per_call\": %.3f, "
                 "\"eager_evals_per_s\": %.4g, \"graph_evals_per_s\": %.4g, \"input_sets\": %d, "
                 "\"kernel_form\": %d}\n",
                 kind, sizeof(T) == 4 ? "f32" : "f64", (long long)B, tiled ? "tiled" : "soa", K, eager_us, host_us,
-                graph_us, B / (eager_us * 1e-6), B / (graph_us * 1e-6), nsets,
+                empty_host_us, graph_us, B / (eager_us * 1e-6), B / (graph_us * 1e-6), nsets,
                 multibody_kernel_form_ex(mb, fd ? 1 : 0, sizeof(T) == 8, B, tiled));
     CHECK_HIP(hipGraphExecDestroy(ge));
     CHECK_HIP(hipGraphDestroy(g));

@@ -357,12 +357,20 @@ hipError_t launch_crba_any(const Multibody *mb, const T *mdl, const T *q, T *H, 
     return rbamd::launch_crba<T>(mb->model.n, mdl, q, H, B, ld, s);
 }
 
-// fwd_kin / jac: the precompiled kernels for serial revolute chains, hipRTC kernels
-// (tree_body.hip.hpp) for trees and prismatic joints.
-// The hipRTC fwd_kin / jac kernel of a tree / prismatic model (serial revolute chains run the
-// precompiled kernels); the launchers and multibody_kernel_path_ex resolve through this one.
+// fwd_kin / jac: the hipRTC kernels (tree_body.hip.hpp fwd_kin_tree / jac_tree, the model's
+// topology and constants compiled in) for every model; serial revolute chains fall back to the
+// precompiled kernels (kinematics.hip) when hipRTC is off or failed.  FR3 2^20: fwd_kin fp64
+// 18.2 vs 26.4 us precompiled, fp32 9.6 vs 11.3; the Jacobian is store-bound, equal (89.2 vs
+// 89.5 / 41.4 vs 41.3 us; profiles/r04/ab/ab_fk*.log, ab_jac*.log).  The launchers and
+// multibody_kernel_path_ex resolve through this one.
 const rbamd::JitKernel *jit_kin(const Multibody *mb, bool jac, bool f64) {
     return jit_get(mb, jac ? rbamd::JitKind::Jac : rbamd::JitKind::FwdKin, f64, !f64 && fast_trig());
+}
+
+// Serial revolute chains take the precompiled kinematics kernels only when the (experimental)
+// tuning `kin_jit` is 0.
+bool kin_precompiled(const Multibody *mb) {
+    return mb->model.serial_revolute() && rbamd::tuning().kin_jit == 0;
 }
 
 template <typename T>
@@ -370,10 +378,10 @@ hipError_t launch_kin_any(const Multibody *mb, bool jac, const T *mdl, const T *
                           hipStream_t s) {
     if (B == 0) return hipSuccess;
     const bool fast = sizeof(T) == 4 && fast_trig();
-    if (mb->model.serial_revolute())
+    const rbamd::JitKernel *jk = kin_precompiled(mb) ? nullptr : jit_kin(mb, jac, sizeof(T) == 8);
+    if (!jk && mb->model.serial_revolute())
         return jac ? rbamd::launch_jac<T>(mb->model.n, mdl, q, out, B, ld, s, fast)
                    : rbamd::launch_fwd_kin<T>(mb->model.n, mdl, q, out, B, ld, s, fast);
-    const rbamd::JitKernel *jk = jit_kin(mb, jac, sizeof(T) == 8);
     if (!jk) return no_generic(mb);
     void *args[] = {(void *)&q, (void *)&out, (void *)&B, (void *)&ld};
     return jit_launch(jk, B, args, s);
@@ -828,7 +836,7 @@ namespace {
 // launchers (launch_*_any).  *generic = true when the precompiled kernel runs (serial revolute
 // fwd_kin / jac, JIT disabled or failed).
 const rbamd::JitKernel *resolve_kernel(const Multibody *mb, int kind, bool f64, int64_t batch, bool tiled) {
-    if (kind >= 4 && mb->model.serial_revolute()) return nullptr;  // precompiled kinematics
+    if (kind >= 4 && kin_precompiled(mb)) return nullptr;  // precompiled kinematics
     if (!rbamd::jit_enabled()) return nullptr;
     const uint32_t B = batch < kChunk ? (uint32_t)batch : (uint32_t)kChunk;
     if (kind == 0) return jit_rnea(mb, f64, fast_trig(), B, tiled);

@@ -45,7 +45,7 @@ std::string literal(double x, bool f64) {
 int jit_nt(JitKind kind) {
     if (kind == JitKind::Rnea) return tuning().rnea_nt & 3;
     if (kind == JitKind::Fd || kind == JitKind::Rollout) return tuning().fd_nt & 3;
-    return 0;
+    return tuning().kin_nt & 3;  // CRBA, fwd_kin, jac
 }
 
 // Rollouts whose K loop must not hoist anything (machine LICM off, the row stride re-derived
@@ -127,7 +127,8 @@ std::string jit_tag(JitKind kind, bool f64, int n) {
     return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n)) +
            ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":r" + std::to_string(tuning().split_rot) + ":v" +
-           std::to_string(tuning().jit_variant) + ":f" + std::to_string(tuning().fd_form);
+           std::to_string(tuning().jit_variant) + ":f" + std::to_string(tuning().fd_form) + ":k" +
+           std::to_string(kind == JitKind::Rnea ? tuning().rnea_park.load() : 0);
 }
 
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req, int tail) {
@@ -189,7 +190,13 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // 131 instead of 125 VGPRs (3 waves/SIMD instead of 4), and all its grid forms (pairs,
     // single tail, one per lane below 2^19) must stay bit-identical to each other.
     const bool dyn = kind == JitKind::Rnea || kind == JitKind::Fd || kind == JitKind::Rollout;
-    if (dyn && !(kind == JitKind::Rnea && f64) && !(tuning().jit_variant & 512)) {
+    const bool com = dyn && !(kind == JitKind::Rnea && f64) && !(tuning().jit_variant & 512);
+    // rnea_lane_park: fp32 one-per-lane RNEA of long serial chains in the centre-of-mass g-form
+    // (signed-permutation frames), when the tuning asks for it
+    const int pk_req = tuning().rnea_park;
+    const int park = (kind == JitKind::Rnea && !f64 && pack == 1 && m.serial_revolute() && com &&
+                      (sr > 0 || (sr < 0 && perm)) && pk_req > 0 && pk_req < m.n) ? pk_req : 0;
+    if (com) {
         o << "#define RB_COM_FORM 1\n";
         o << "static __device__ constexpr double rb_com[" << 9 * m.n << "] = {\n";
         for (int i = 0; i < m.n; ++i) {
@@ -297,6 +304,15 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << seq_prologue;
         o << "  rbamd::dev::rnea_lane_seq2<T, N, " << F
           << ", Topo>(kModel, q + oA, qd + oA, qdd + oA, tau + oA, offA, offB, twoB, ld);\n}\n";
+    } else if (kind == JitKind::Rnea && park > 0) {
+        o << "extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void "
+             "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+             "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+        o << "  rbamd::dev::rnea_lane_park<T, N, " << F << ", " << park
+          << ">(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n}\n";
     } else if (kind == JitKind::Rnea) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";

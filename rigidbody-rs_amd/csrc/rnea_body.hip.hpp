@@ -187,6 +187,76 @@ __device__ __forceinline__ void rnea_lane_seq2(const T *mdl, const T *__restrict
     if (two) rnea_any<T, N, FAST, Topo>(mdl, qb, qdb, qddb, [&](int j, T v) { st_row(tau, j * ld, offB, v); });
 }
 
+// Long serial chains in fp32 (jit rnea_park = NP > 0, model-specialised, centre-of-mass g-form):
+// the same arithmetic as rnea_eval with fewer live values, for 3 waves per SIMD where rnea_lane
+// holds ~240 (30 links: per link n, g and (cos, sin) -- 246 VGPRs, 2 waves/SIMD).
+//   * the first NP links' (n, g) go to LDS during the forward sweep (the backward sweep needs
+//     them last): NP x 6 rows x 64 lanes x 4 B per wave (NP = 8: 12 KB, 12 waves per CU);
+//   * (cos, sin) are not kept: the backward sweep reloads q_j (a row the lane read moments
+//     before -- an L2 / Infinity Cache hit) D links ahead and re-evaluates the same sincos, so
+//     every value equals rnea_eval's bit for bit.
+template <typename T, int N, bool FAST, int NP>
+__device__ __forceinline__ void rnea_lane_park(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                               const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b,
+                                               int64_t ld) {
+    static_assert(kRneaGForm && NP > 0 && NP < N, "centre-of-mass g-form serial chains only");
+    constexpr int D = 4;  // backward-sweep reload distance (links)
+    __shared__ T park[4][NP * 6][64];
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    T qv[N], qdv[N], qddv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {  // q temporal: the backward sweep reads it again
+        qv[j] = ld_row<T, false>(q, j * ld, off);
+        qdv[j] = ld_row(qd, j * ld, off);
+        qddv[j] = ld_row(qdd, j * ld, off);
+    }
+    V3<T> fn[N], gg[N];  // entries j < NP live in LDS after the forward sweep
+    auto put = [&](int j) {
+        const T v[6] = {fn[j].x, fn[j].y, fn[j].z, gg[j].x, gg[j].y, gg[j].z};
+#pragma unroll
+        for (int k = 0; k < 6; ++k) park[w][6 * j + k][l] = v[k];
+    };
+    RneaState<T> st;
+    T sn, cs;
+    rnea_fwd0<T, FAST, true>(mdl, qv[0], qdv[0], qddv[0], st, sn, cs, fn[0], gg[0]);
+    put(0);
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+        rnea_fwd<T, FAST, true>(mdl, j, qv[j], qdv[j], qddv[j], st, sn, cs, fn[j], gg[j]);
+        if (j < NP) put(j);
+    }
+    reload_fence();
+    T qr[N];
+#pragma unroll
+    for (int j = N - 1; j >= N - D && j >= 1; --j) qr[j] = ld_row<T, false>(q, j * ld, off);
+    __builtin_amdgcn_sched_barrier(0);
+    // rnea_bwd_g (above) with (cos, sin) from the reloaded q and the first links' forces from LDS
+    const T ml = load_link(mdl, N - 1).m;
+    V3<T> F = v3(ml * gg[N - 1].x, ml * gg[N - 1].y, ml * gg[N - 1].z);
+    V3<T> n = fn[N - 1];
+#pragma unroll
+    for (int j = N - 1; j >= 1; --j) {
+        st_row(tau, j * ld, off, n.z);
+        if (j - D >= 1) qr[j - D] = ld_row<T, false>(q, (j - D) * ld, off);
+        T s, c;
+        sin_cos<FAST>(qr[j], s, c);
+        const Link<T> L = load_link(mdl, j);
+        const M3<T> E = joint_rotation(L.Rp, c, s);
+        const V3<T> fl = mul(E, F);
+        V3<T> fp = fn[j - 1], gp = gg[j - 1];
+        if (j - 1 < NP) {
+            fp = v3(park[w][6 * (j - 1) + 0][l], park[w][6 * (j - 1) + 1][l], park[w][6 * (j - 1) + 2][l]);
+            gp = v3(park[w][6 * (j - 1) + 3][l], park[w][6 * (j - 1) + 4][l], park[w][6 * (j - 1) + 5][l]);
+        }
+        const T mp = load_link(mdl, j - 1).m;
+        F = v3(fmadd(mp, gp.x, fl.x), fmadd(mp, gp.y, fl.y), fmadd(mp, gp.z, fl.z));
+        n = cross_add(mul_add(fp, E, n), L.p, fl);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    st_row(tau, 0, off, n.z);
+}
+
 // Streaming form (precompiled generic kernels, rnea.hip): walk the batch with `stride`,
 // prefetching the next configuration's joint values into registers before evaluating the
 // current one.

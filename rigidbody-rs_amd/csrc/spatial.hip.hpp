@@ -138,6 +138,7 @@ struct SerialTopo {
     static constexpr bool kSerial = true;
     static constexpr int parent(int j) { return j - 1; }
     static constexpr bool prismatic(int) { return false; }
+    static constexpr bool on_path(int) { return true; }  // every link is an ancestor of the last
 };
 
 // Per-link model constants.  Each workgroup first copies the packed block (layout.hpp,
@@ -324,9 +325,13 @@ RB_HD void link_force(const Link<T> &L, int, const V3<T> &w, const V3<T> &v, con
 template <typename T>
 using gptr = __attribute__((address_space(1))) T *;
 
-template <typename T>
+// NTL = false: a temporal load whatever RB_NT says (a row the lane will read again).
+template <typename T, bool NTL = (RB_NT & 1) != 0>
 __device__ __forceinline__ T ld_row(const T *__restrict__ base, int64_t row, uint32_t off) {
-    if constexpr ((RB_VARIANT & 64) != 0) {
+    if constexpr (!NTL) {
+        gptr<const T> p = (gptr<const T>)((gptr<const char>)(base + row) + off);
+        return *p;
+    } else if constexpr ((RB_VARIANT & 64) != 0) {
         const T *p = reinterpret_cast<const T *>(reinterpret_cast<const char *>(base + row) + off);
         if constexpr ((RB_NT & 1) != 0) return __builtin_nontemporal_load(p);
         return *p;

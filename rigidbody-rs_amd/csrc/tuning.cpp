@@ -47,6 +47,9 @@ const Key kKeys[] = {
     {"split_rot", &Tuning::split_rot, true},
     {"jit_variant", &Tuning::jit_variant, true},
     {"seq_tail", &Tuning::seq_tail, true},
+    {"kin_jit", &Tuning::kin_jit, true},
+    {"kin_nt", &Tuning::kin_nt, true},
+    {"rnea_park", &Tuning::rnea_park, true},
 };
 
 // RB_<KEY> environment overrides (upper-cased key), experimental ones only with RB_EXPERIMENTAL=1.

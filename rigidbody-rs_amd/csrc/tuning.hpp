@@ -67,6 +67,16 @@ struct Tuning {
     // -1 auto: 75 for the tiled layout (FR3 fp64 2^20: 40.5 vs 41.8 us), 0 for SoA (43.6-45.9 vs
     // 42.9 us), DESIGN.md §4.
     std::atomic<int> seq_tail{-1};
+    // Batched fwd_kin / jac of serial revolute chains: 1 = the model-specialised hipRTC kernels
+    // (tree_body.hip.hpp fwd_kin_tree / jac_tree with the chain's topology), 0 = the precompiled
+    // kernels (kinematics.hip), -1 auto (the hipRTC kernels: fwd_kin fp64 18.2 vs 26.4 us at 2^20).
+    std::atomic<int> kin_jit{-1};
+    // JIT fp32 RNEA of serial chains longer than this many links: the first `rnea_park` links'
+    // forces parked in LDS and (cos, sin) re-evaluated from reloaded q (rnea_body.hip.hpp
+    // rnea_lane_park) for 3 waves/SIMD; 0 = off.
+    std::atomic<int> rnea_park{0};
+    // JIT CRBA / fwd_kin / jac: same bits as rnea_nt.
+    std::atomic<int> kin_nt{0};
 };
 
 // Process-wide knobs, initialised from RB_JIT / RB_PACK / RB_RNEA_STREAM (and, with

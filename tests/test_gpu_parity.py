@@ -323,18 +323,22 @@ def test_full_size_properties(ffi, dev, fr3_text):
 # ------------------------------------------------------------ JIT vs generic
 @pytest.mark.parametrize("name", ["fr3_golden.npz", "chain30_golden.npz"])
 def test_jit_and_generic_kernels_agree(name, ffi, dev, fr3_text):
-    """Both RNEA code paths -- model-specialised (hipRTC) and precompiled generic --
-    meet the oracle tolerance; the JIT path is really taken when enabled."""
+    """Both code paths -- model-specialised (hipRTC) and precompiled generic -- meet the
+    oracle tolerance for RNEA, forward dynamics, CRBA and the kinematics (fwd_kin / jac, whose
+    serial-chain default is the hipRTC kernel since round 4); the JIT path is really taken when
+    enabled."""
     g = load_npz(name)
     mb = ffi.Multibody.from_urdf_string(_model_xml(name, fr3_text))
     om = _oracle(_model_xml(name, fr3_text))
     try:
         for jit in (1, 0):
             ffi.set_tuning("jit", jit)
-            for kind in ("rnea", "fd", "crba"):
+            for kind in ("rnea", "fd", "crba", "fwd_kin", "jac"):
                 for f64 in (False, True):
                     assert mb.kernel_path(kind, f64) == ("jit" if jit else "generic"), ffi.last_error()
             q, qd, qdd = (_t(g[k], dev) for k in ("q", "qd", "qdd"))
+            _close(mb.fwd_kin_batch(q).cpu().numpy(), g["pos"], 1e-9, f"fwd_kin f64 jit={jit}")
+            _close(mb.jac_batch(q).cpu().numpy(), g["J"], 1e-9, f"jac f64 jit={jit}")
             _close(mb.rnea_batch(q, qd, qdd).cpu().numpy(), g["tau"], 1e-9, f"rnea f64 jit={jit}")
             q32, qd32, qdd32 = (x.float() for x in (q, qd, qdd))
             ref = om.rnea_batch(*[x.double().cpu().numpy() for x in (q32, qd32, qdd32)])

@@ -49,6 +49,8 @@ def main():
     for lay in a.layouts:
         if a.kernel == "rollout":
             launches[lay] = bench.rollout_launcher(mb, a.batch, dtype, a.rollout_k)
+        elif a.kernel in bench.Q_KERNELS:  # crba / jac / fwd_kin: q in, SoA only
+            launches[lay] = bench.q_launcher(mb, a.kernel, a.batch, dtype, 1.25)[0]
         else:
             sets = bench.make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED, lay)
             launches[lay] = bench.batch_launcher(mb, sets, a.kernel, dtype, lay, a.batch)
@@ -56,7 +58,7 @@ def main():
     # every knob any variant sets is reset to the library default (tuning.hpp) before each
     # variant, so a knob of one variant never leaks into the next
     defaults = {"rnea_stream": -1, "grid_factor": 1, "jit": 1, "rnea_nt": 3, "fd_nt": 3, "jit_waves": -1,
-                "opaque_consts": -1, "pack": -1, "f64_tab": -1, "split_rot": -1, "jit_variant": 0, "seq_tail": -1,
+                "opaque_consts": -1, "pack": -1, "f64_tab": -1, "split_rot": -1, "jit_variant": 0, "seq_tail": -1, "kin_jit": -1, "kin_nt": 0, "rnea_park": 0,
                 "fd_form": -1}
     used = {kv.split("=")[0] for v in a.variants for kv in v.split(",")} - {"streams"}
     keys = [(v, lp) for v in a.variants for lp in launches]

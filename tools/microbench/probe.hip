@@ -97,7 +97,7 @@ hipError_t probe_nt(const float *in, float *out, uint32_t B, int64_t ld, int wid
 }
 }  // namespace
 
-// Row shapes of the dynamics kernels: 7-DOF (21 in / 7 out), 12-DOF, 30-DOF, and 4/4.
+// Row shapes of the dynamics kernels: 7-DOF (21 in / 7 out), 12-DOF, 30-DOF, 4/4, and the q-only kernels.
 hipError_t launch_probe_rows(const float *in, float *out, int rows_in, int rows_out, uint32_t B, int64_t ld,
                              int width, hipStream_t s) {
     if (B == 0) return hipSuccess;
@@ -110,6 +110,11 @@ hipError_t launch_probe_rows(const float *in, float *out, int rows_in, int rows_
     if (rows_in == 36 && rows_out == 12) return probe_nt<36, 12>(in, out, B, ld, width, nt, s);
     if (rows_in == 90 && rows_out == 30) return probe_nt<90, 30>(in, out, B, ld, width, nt, s);
     if (rows_in == 4 && rows_out == 4) return probe_nt<4, 4>(in, out, B, ld, width, nt, s);
+    // the q-only kernels of FR3: CRBA (7 in / 49 out), Jacobian (7 / 42), forward
+    // kinematics (7 / 3)
+    if (rows_in == 7 && rows_out == 49) return probe_nt<7, 49>(in, out, B, ld, width, nt, s);
+    if (rows_in == 7 && rows_out == 42) return probe_nt<7, 42>(in, out, B, ld, width, nt, s);
+    if (rows_in == 7 && rows_out == 3) return probe_nt<7, 3>(in, out, B, ld, width, nt, s);
     return hipErrorInvalidValue;
 }
 

@@ -43,7 +43,13 @@ def run(rows_in, rows_out, width, nt=0, B=1 << 20, steps=100, rounds=5):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "chain30":
+    if len(sys.argv) > 1 and sys.argv[1] == "qkernels":
+        # FR3 CRBA / Jacobian / forward-kinematics shapes in fp64 (2^20 configurations = 2^21
+        # floats per row, 8 B per lane) and fp32 (2^20 floats, 4 B per lane), SoA, with and
+        # without non-temporal stores
+        out = [run(7, ro, w, nt, B=B) for ro in (49, 42, 3) for (w, B) in ((2, 1 << 21), (1, 1 << 20))
+               for nt in (0, 2, 3)]
+    elif len(sys.argv) > 1 and sys.argv[1] == "chain30":
         # the 30-DOF RNEA shape (90 rows in / 30 out), SoA and tiled, with / without nt
         out = [run(90, 30, 1, nt, B=1 << 20) for nt in (0, 3, 4, 7)]
     elif len(sys.argv) > 1 and sys.argv[1] == "tiled":
