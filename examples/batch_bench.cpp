@@ -137,6 +137,7 @@ int run(const char *kind, int64_t B, int K, bool tiled) {
     // the runtime's floor: K launches of an empty kernel of the same grid from this thread
     const unsigned grid = (unsigned)((B + 255) / 256);
     for (int i = 0; i < 100; ++i) hipLaunchKernelGGL(empty_kernel, dim3(grid), dim3(256), 0, st, nullptr);
+    CHECK_HIP(hipGetLastError());
     CHECK_HIP(hipStreamSynchronize(st));
     auto g0 = std::chrono::steady_clock::now();
     for (int i = 0; i < K; ++i) hipLaunchKernelGGL(empty_kernel, dim3(grid), dim3(256), 0, st, nullptr);

@@ -45,7 +45,9 @@ std::string literal(double x, bool f64) {
 int jit_nt(JitKind kind) {
     if (kind == JitKind::Rnea) return tuning().rnea_nt & 3;
     if (kind == JitKind::Fd || kind == JitKind::Rollout) return tuning().fd_nt & 3;
-    return tuning().kin_nt & 3;  // CRBA, fwd_kin, jac
+    const int v = tuning().kin_nt;  // CRBA, fwd_kin, jac
+    if (v >= 0) return v & 3;
+    return kind == JitKind::FwdKin ? 3 : 2;  // 7 rows in / 3 out: non-temporal loads pay too
 }
 
 // Rollouts whose K loop must not hoist anything (machine LICM off, the row stride re-derived
@@ -193,7 +195,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     const bool com = dyn && !(kind == JitKind::Rnea && f64) && !(tuning().jit_variant & 512);
     // rnea_lane_park: fp32 one-per-lane RNEA of long serial chains in the centre-of-mass g-form
     // (signed-permutation frames), when the tuning asks for it
-    const int pk_req = tuning().rnea_park;
+    const int pk_req = tuning().rnea_park < 0 ? (m.n >= 20 ? 8 : 0) : tuning().rnea_park.load();
     const int park = (kind == JitKind::Rnea && !f64 && pack == 1 && m.serial_revolute() && com &&
                       (sr > 0 || (sr < 0 && perm)) && pk_req > 0 && pk_req < m.n) ? pk_req : 0;
     if (com) {

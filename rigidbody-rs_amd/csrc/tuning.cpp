@@ -38,6 +38,7 @@ const Key kKeys[] = {
     {"rnea_stream", &Tuning::rnea_stream, false},
     {"single_gpu", &Tuning::single_gpu, false},
     {"fd_form", &Tuning::fd_form, false},
+    {"rnea_park", &Tuning::rnea_park, false},
     {"grid_factor", &Tuning::grid_factor, true},
     {"rnea_nt", &Tuning::rnea_nt, true},
     {"fd_nt", &Tuning::fd_nt, true},
@@ -49,7 +50,6 @@ const Key kKeys[] = {
     {"seq_tail", &Tuning::seq_tail, true},
     {"kin_jit", &Tuning::kin_jit, true},
     {"kin_nt", &Tuning::kin_nt, true},
-    {"rnea_park", &Tuning::rnea_park, true},
 };
 
 // RB_<KEY> environment overrides (upper-cased key), experimental ones only with RB_EXPERIMENTAL=1.

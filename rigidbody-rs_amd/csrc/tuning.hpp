@@ -1,7 +1,7 @@
 // tuning.hpp -- launch-shape knobs (host side) and resident-grid sizing.
 //
 // Production knobs (rb_set_tuning accepts these always): `jit`, `pack`, `rnea_stream`,
-// `single_gpu`, `fd_form`.
+// `single_gpu`, `fd_form`, `rnea_park`.
 // Everything else is an A/B experiment selector: rb_set_tuning accepts it only when the
 // process runs with RB_EXPERIMENTAL=1 (tools/ab_bench.py, tools/small_batch.py), so a normal
 // caller cannot multiply the hipRTC kernel variants (jit.cpp cache key) or the test matrix.
@@ -35,6 +35,11 @@ struct Tuning {
     // RNEA, H by CRBA, L D L^T solve -- the oracle's own definition), -1 auto (jit.cpp
     // jit_fd_form: mass matrix for serial chains up to 8 links).
     std::atomic<int> fd_form{-1};
+    // JIT fp32 RNEA of long serial chains: the first `rnea_park` links' forces parked in LDS and
+    // (cos, sin) re-evaluated from reloaded q (rnea_body.hip.hpp rnea_lane_park), 3 waves/SIMD
+    // instead of 2; 0 = off, -1 auto (8 for chains of 20+ links: 30-link 2^20 91.0 vs 103.4 us,
+    // bit-identical).
+    std::atomic<int> rnea_park{-1};
 
     // ---- experimental (RB_EXPERIMENTAL=1)
     std::atomic<int> grid_factor{1};  // streaming grid = grid_factor x resident blocks (capped by the batch)
@@ -71,12 +76,11 @@ struct Tuning {
     // (tree_body.hip.hpp fwd_kin_tree / jac_tree with the chain's topology), 0 = the precompiled
     // kernels (kinematics.hip), -1 auto (the hipRTC kernels: fwd_kin fp64 18.2 vs 26.4 us at 2^20).
     std::atomic<int> kin_jit{-1};
-    // JIT fp32 RNEA of serial chains longer than this many links: the first `rnea_park` links'
-    // forces parked in LDS and (cos, sin) re-evaluated from reloaded q (rnea_body.hip.hpp
-    // rnea_lane_park) for 3 waves/SIMD; 0 = off.
-    std::atomic<int> rnea_park{0};
-    // JIT CRBA / fwd_kin / jac: same bits as rnea_nt.
-    std::atomic<int> kin_nt{0};
+    // JIT CRBA / fwd_kin / jac: same bits as rnea_nt; -1 auto = 2 for CRBA and jac
+    // (non-temporal stores: the outputs are written once; FR3 2^20 fp64 CRBA 84.7 vs 102.9 us,
+    // jac 70.3 vs 89.3, fp32 CRBA 40.5 vs 46.2 -- at the no-math probe's 5.9 TB/s for these row
+    // shapes), 3 for fwd_kin (16.4 vs 17.2 with stores only, 18.3 with neither).
+    std::atomic<int> kin_nt{-1};
 };
 
 // Process-wide knobs, initialised from RB_JIT / RB_PACK / RB_RNEA_STREAM (and, with

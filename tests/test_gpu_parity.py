@@ -281,6 +281,37 @@ def test_chain30_full_size_f32(ffi, dev):
           f"affine {worst_aff:.2e}, fd32 backward K {K:.1f}")
 
 
+def test_rnea_park_bit_identical(ffi, dev):
+    """The parked long-chain fp32 RNEA (tuning rnea_park, rnea_body.hip.hpp rnea_lane_park: the
+    first links' forces in LDS, (cos, sin) re-evaluated from reloaded q; the default for chains
+    of 20+ links) is rnea_eval's arithmetic: bit-identical to rnea_park = 0 on the 30-DOF chain,
+    ragged and full batches, SoA (ld > B, padding untouched) and tiled."""
+    from rigidbody_amd import chains
+
+    mb = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
+    n, lim = mb.n, mb.limits()
+    for B in (1, 63, 1000, 65539, 1 << 20):
+        ld = B + 3
+        full = [torch.full((n, ld), 5.0, dtype=torch.float32, device=dev) for _ in range(3)]
+        for k, kind in enumerate(("q", "qd", "qdd")):
+            full[k][:, :B] = _t(chains.host_uniform(n, B, *chains.input_ranges(lim, kind), chains.SEED + 60 + k,
+                                                    dtype="float32"), dev, torch.float32)
+        x = [f[:, :B] for f in full]
+        res = {}
+        try:
+            for park in (-1, 0):
+                ffi.set_tuning("rnea_park", park)
+                out = torch.full((n, ld), 123.0, dtype=torch.float32, device=dev)
+                mb.rnea_batch(*x, out=out[:, :B])
+                assert torch.all(out[:, B:] == 123.0), (B, park)
+                til = ffi.from_tiled(mb.rnea_batch_tiled(*[ffi.to_tiled(a.contiguous()) for a in x], B), B)
+                res[park] = (out[:, :B].cpu().numpy(), til.cpu().numpy())
+        finally:
+            ffi.set_tuning("rnea_park", -1)
+        np.testing.assert_array_equal(res[-1][0], res[0][0], err_msg=f"B={B} soa")
+        np.testing.assert_array_equal(res[-1][1], res[0][1], err_msg=f"B={B} tiled")
+
+
 def test_full_size_properties(ffi, dev, fr3_text):
     """BASELINE config size (fr3, B = 2^20): the oracle cannot cover every column, so
     check size-independent properties on all of them plus an oracle spot check:
