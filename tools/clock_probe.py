@@ -41,7 +41,7 @@ CASES = [
     ("fd_fr3_f32", "fd", False, 7, 4, 2, -1),
     ("fd_fr3_f32_p4", "fd", False, 7, 8, 1, 4),  # small-batch split: waves 0/1 bias, 2/3 mass matrix
     ("rnea_fr3_f32", "rnea", False, 7, 8, 1, -1),
-    ("rnea_chain30_f32", "rnea", False, 30, 2, 1, -1),
+    ("rnea_chain30_f32", "rnea", False, 30, 3, 1, -1),  # parked forces (rnea_lane_park): 3 waves/SIMD
 ]
 
 

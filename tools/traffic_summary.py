@@ -55,6 +55,9 @@ def main():
     B = int(workload.rsplit("_b", 1)[1])
     es = 4 if "_f32_" in workload else 8
     alg = (8 if workload.startswith("rnea_fd") else 4) * n * es * B
+    q_rows = {"crba": n * n, "jac": 6 * n, "fwd": 3}.get(workload.split("_")[0])
+    if q_rows is not None:  # q-only kernels: n rows read, n*n / 6n / 3 rows written
+        alg = (n + q_rows) * es * B
     if workload.startswith("rollout_"):  # K steps: K tau rows read, q and qd read and written
         K = int(workload.split("_K")[1].split("_")[0])
         alg = (K + 4) * n * es * B
