@@ -159,9 +159,8 @@ int multibody_fd_batch_f64(const Multibody *mb, const double *q, const double *q
 /* Tiled layout (same computation): every array is [ceil(batch/256)][rows][256], element
  * (row j, configuration b) at ((b / 256) * rows + j) * 256 + b % 256, rows = n -- each
  * 256-configuration tile of all joints contiguous.  Measured on MI355X (bench.py layout_ab_*
- * lines, interleaved in one process, driver runs): fp64 RNEA 3-4% faster than SoA rows, fp32
- * RNEA 0-6% faster (its SoA / tiled order moves with the memory power state across runs), fp64
- * FD equal -- use it when the data is produced tiled, not by converting.  Allocate
+ * lines, interleaved in one process, driver runs): fp64 RNEA 3-6% faster than SoA rows, fp32
+ * RNEA ~5% faster, fp64 FD equal -- use it when the data is produced tiled, not by converting.  Allocate
  * whole tiles; lanes past `batch` in the last tile are neither read nor written. */
 int multibody_rnea_batch_tiled_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
                                    float *tau, int64_t batch, void *stream);

@@ -97,7 +97,7 @@ struct Multibody {
         const rbamd::JitKernel *jk = nullptr;
     };
     mutable std::map<std::pair<const void *, const rbamd::JitKernel *>, JitPub> jit_pub;
-    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][6][2] = {};
+    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][6][4] = {};  // last: tail > 0, nt override
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
@@ -178,14 +178,14 @@ int device_consts(const Multibody *mb, const T **out) {
 // pack: configurations per lane, 0 = the jit_pack policy (jit.cpp).
 // tail: percent of a sequential-pair RNEA launch run one per lane (jit_seq_tail); other kinds 0.
 const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f64, bool fast, int pack = 0,
-                                int tail = 0) {
+                                int tail = 0, int nt = -1) {
     if (!rbamd::jit_enabled()) return nullptr;
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
     const bool fst = fast && !f64;
     std::atomic<const Multibody::JitPub *> *slot = nullptr;
     if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 6) {
-        slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][tail > 0 ? 1 : 0];
+        slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][(tail > 0 ? 1 : 0) | (nt >= 0 ? 2 : 0)];
         if (const Multibody::JitPub *p = slot->load(std::memory_order_acquire))
             if (p->gen.load(std::memory_order_acquire) == rbamd::tuning_generation()) return p->jk;
     }
@@ -201,10 +201,10 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
         const int tl = (kind == rbamd::JitKind::Rnea && pk == 3) ? tail : 0;
         const std::string key = std::to_string(d) + ":k" + std::to_string((int)kind) + (f64 ? ":f64" : ":f32") +
                                 (fst ? ":fast" : ":precise") + rbamd::jit_tag(kind, f64, mb->model.n) + ":q" +
-                                std::to_string(pk) + ":st" + std::to_string(tl);
+                                std::to_string(pk) + ":st" + std::to_string(tl) + ":n" + std::to_string(nt);
         auto it = mb->jit.find(key);
         if (it == mb->jit.end()) {
-            rbamd::JitKernel built = rbamd::jit_build(mb->model, kind, f64, fst, pk, tl);
+            rbamd::JitKernel built = rbamd::jit_build(mb->model, kind, f64, fst, pk, tl, nt);
             if (rbamd::tuning_generation() != gen) {  // the tuning moved under the build
                 if (built.module) (void)hipModuleUnload(built.module);
                 continue;
@@ -231,7 +231,10 @@ constexpr uint32_t kSeqMinBatch = 1u << 19;
 
 const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast, uint32_t B, bool tiled) {
     const int pack = (rbamd::tuning().pack < 0 && B < kSeqMinBatch) ? 1 : 0;
-    return jit_get(mb, rbamd::JitKind::Rnea, f64, fast, pack, rbamd::jit_seq_tail(tiled));
+    // fp32 on the tiled layout at large batches: ordinary (temporal) loads and stores
+    // (tuning.hpp rnea_nt)
+    const int nt = (!f64 && tiled && B >= kSeqMinBatch && rbamd::tuning().rnea_nt < 0) ? 0 : -1;
+    return jit_get(mb, rbamd::JitKind::Rnea, f64, fast, pack, rbamd::jit_seq_tail(tiled), nt);
 }
 
 // A tree / prismatic model has no precompiled kernel: without its hipRTC kernel the launch

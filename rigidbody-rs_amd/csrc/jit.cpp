@@ -43,7 +43,7 @@ std::string literal(double x, bool f64) {
 }  // namespace
 
 int jit_nt(JitKind kind) {
-    if (kind == JitKind::Rnea) return tuning().rnea_nt & 3;
+    if (kind == JitKind::Rnea) return tuning().rnea_nt < 0 ? 3 : (tuning().rnea_nt & 3);
     if (kind == JitKind::Fd || kind == JitKind::Rollout) return tuning().fd_nt & 3;
     const int v = tuning().kin_nt;  // CRBA, fwd_kin, jac
     if (v >= 0) return v & 3;
@@ -133,7 +133,7 @@ std::string jit_tag(JitKind kind, bool f64, int n) {
            std::to_string(kind == JitKind::Rnea ? tuning().rnea_park.load() : 0);
 }
 
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req, int tail) {
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req, int tail, int nt) {
     std::vector<double> pk = m.pack_f64();
     for (int i = 0; i < m.n; ++i) {
         double *c = &pk[(size_t)i * kLinkStride];
@@ -144,7 +144,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     const int pack = jit_model_pack(m, kind, f64, pack_req);
     const bool fdh = kind == JitKind::Fd && jit_fd_form(m) == 2;
     std::ostringstream o;
-    o << "#define RB_NT " << jit_nt(kind) << "\n";
+    o << "#define RB_NT " << (nt >= 0 ? nt : jit_nt(kind)) << "\n";
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
     o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
     if (kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack)) o << "#define RB_ROLLOUT_NO_HOIST 1\n";
@@ -392,8 +392,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
 }
 
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
-                 std::vector<char> *code, std::string *error, int pack, int tail) {
-    const std::string src = jit_source(m, kind, f64, fast, pack, tail);
+                 std::vector<char> *code, std::string *error, int pack, int tail, int nt) {
+    const std::string src = jit_source(m, kind, f64, fast, pack, tail, nt);
     hiprtcProgram prog = nullptr;
     if (hiprtcCreateProgram(&prog, src.c_str(), "rb_jit.hip", kJitHeaderCount, kJitHeaderSources,
                             kJitHeaderNames) != HIPRTC_SUCCESS) {
@@ -443,7 +443,7 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     return true;
 }
 
-JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack, int tail) {
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack, int tail, int nt) {
     JitKernel jk;
     jk.pack = jit_model_pack(m, kind, f64, pack);
     if (kind == JitKind::Rnea && jk.pack == 3) jk.seq_tail = tail > 0 ? tail : 0;
@@ -454,7 +454,7 @@ JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack,
         return jk;
     }
     std::vector<char> code;
-    if (!jit_compile(m, kind, f64, fast, prop.gcnArchName, &code, &jk.error, jk.pack, jk.seq_tail)) return jk;
+    if (!jit_compile(m, kind, f64, fast, prop.gcnArchName, &code, &jk.error, jk.pack, jk.seq_tail, nt)) return jk;
     hipError_t e = hipModuleLoadData(&jk.module, code.data());
     if (e != hipSuccess) {
         jk.error = std::string("hipModuleLoadData: ") + hipGetErrorString(e);

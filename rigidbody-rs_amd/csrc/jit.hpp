@@ -41,7 +41,8 @@ bool jit_enabled();
 // Generated HIP source for one specialised kernel (exposed for tests / inspection).
 // pack: configurations per lane, 0 = the jit_pack policy.
 // tail: sequential-pair RNEA only -- percent of the launch's tiles run one per lane (0 none).
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0);
+// nt: the non-temporal load / store bits compiled in (RB_NT); -1 = jit_nt(kind).
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0, int nt = -1);
 
 // Non-temporal access bits of `kind`'s JIT source, and the cache-key suffix of every
 // tuning value that changes the source (tuning.hpp).
@@ -62,9 +63,10 @@ int jit_seq_tail(bool tiled);
 
 // hipRTC compilation only (no device needed): fills `code` with the code object.
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
-                 std::vector<char> *code, std::string *error, int pack = 0, int tail = 0);
+                 std::vector<char> *code, std::string *error, int pack = 0, int tail = 0,
+                 int nt = -1);
 
 // Compiles and loads the kernel on the current device.  Never throws.
-JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0);
+JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0, int nt = -1);
 
 }  // namespace rbamd

@@ -66,7 +66,7 @@ def main():
         sets = bench.make_sets(mb, a.batch, dtype, k, ns, chains.SEED, "tiled")
         for v in a.variants:
             launches[f"{k}:{v}"] = (bench.batch_launcher(mb, sets, k, dtype, "tiled", a.batch), v)
-    defaults = {"rnea_stream": -1, "grid_factor": 1, "jit": 1, "rnea_nt": 3, "fd_nt": 3, "jit_waves": -1,
+    defaults = {"rnea_stream": -1, "grid_factor": 1, "jit": 1, "rnea_nt": -1, "fd_nt": 3, "jit_waves": -1,
                 "opaque_consts": -1, "pack": -1, "f64_tab": -1, "split_rot": -1, "jit_variant": 0}
     res = {k: [] for k in launches}
     for r in range(a.rounds):
