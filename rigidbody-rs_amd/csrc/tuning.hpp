@@ -45,9 +45,10 @@ struct Tuning {
     std::atomic<int> grid_factor{1};  // streaming grid = grid_factor x resident blocks (capped by the batch)
     // JIT RNEA: bit 0 non-temporal loads, bit 1 non-temporal stores (every element is
     // touched once; fp64 FR3 2^20 tiled 39.9 vs 42.7 us without, 30-DOF 91.4 vs 98.6, 65536
-    // fp32 3.46 vs 3.89); -1 auto = 3, except 0 for the fp32 RNEA of batches >= 2^19 on the tiled
-    // layout (FR3 2^20: 22.4 vs 25.2 us, steady where nt=3 swings 20-25; SoA rows keep 3: 24.3
-    // vs 24.9) -- capi.cpp jit_rnea.
+    // fp32 3.46 vs 3.89); -1 auto = 3, except 0 for the fp32 RNEA of chains up to 8 links at
+    // batches >= 2^19 on the tiled layout (FR3 2^20: 22.4 vs 25.2 us, steady where nt=3 swings
+    // 20-25; SoA rows keep 3: 24.3 vs 24.9; the 30-link chain 99.9 vs 91.3 and the 14-DOF tree
+    // 44.2 vs 41.2 keep 3) -- capi.cpp jit_rnea.
     std::atomic<int> rnea_nt{-1};
     // JIT forward dynamics / rollout: same bits as rnea_nt (-5% fp32 FD kernel time).
     std::atomic<int> fd_nt{3};
