@@ -866,7 +866,7 @@ void note_jit_errors(const Multibody *mb) {
 int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled) {
     if (int rc = check_kernel_query(mb, kind, batch)) return -rc;
     if (resolve_kernel(mb, kind, f64 != 0, batch, tiled != 0)) return 1;
-    if (rbamd::jit_enabled() && !(kind >= 4 && mb->model.serial_revolute())) note_jit_errors(mb);
+    if (rbamd::jit_enabled() && !(kind >= 4 && kin_precompiled(mb))) note_jit_errors(mb);
     return 0;
 }
 

@@ -571,14 +571,16 @@ def test_paired_rollout_vs_single_and_oracle(B, ffi, dev, fr3_text):
 def test_tiled_layout_matches_soa_bitwise(name, ffi, dev, fr3_text):
     """The tiled [ceil(B/256), n, 256] entry points run the same lane arithmetic as the
     SoA ones: outputs are bit-identical (JIT and generic kernels, fp32 and fp64, ragged
-    batches), the layout conversions are exact round trips, and the oracle agrees."""
+    batches), the layout conversions are exact round trips, and the oracle agrees.  From 2^19
+    the fp32 FR3 tiled launch compiles without non-temporal loads / stores (tuning rnea_nt auto)
+    while the SoA launch keeps them: still the same arithmetic, bit for bit."""
     mb = ffi.Multibody.from_urdf_string(_model_xml(name, fr3_text))
     om = _oracle(_model_xml(name, fr3_text))
     n = mb.n
     try:
         for jit in (1, 0):
             ffi.set_tuning("jit", jit)
-            for B in (1, 255, 256, 1000, 65536 + 3):
+            for B in (1, 255, 256, 1000, 65536 + 3, (1 << 19) + 5):
                 rng = np.random.default_rng(B)
                 q, qd, qdd = (rng.uniform(-2, 2, (n, B)) for _ in range(3))
                 for dt in (torch.float64, torch.float32):
