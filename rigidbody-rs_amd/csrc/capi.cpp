@@ -230,10 +230,13 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
 constexpr uint32_t kSeqMinBatch = 1u << 19;
 
 const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast, uint32_t B, bool tiled) {
-    const int pack = (rbamd::tuning().pack < 0 && B < kSeqMinBatch) ? 1 : 0;
-    // fp32 chains up to 8 links on the tiled layout at large batches: ordinary (temporal) loads
-    // and stores (tuning.hpp rnea_nt; the 30-link chain and the 14-DOF tree keep nt = 3)
-    const int nt = (!f64 && tiled && B >= kSeqMinBatch && mb->model.n <= 8 && rbamd::tuning().rnea_nt < 0) ? 0 : -1;
+    // fp32 chains up to 8 links on the tiled layout at large batches: the sequential pair too
+    // (FR3 2^20 22.0-22.1 vs 22.3-24.0 us on two boxes, profiles/r04/ab/ab_r32_seq*.log), with
+    // ordinary (temporal) loads and stores (tuning.hpp rnea_nt; the 30-link chain and the 14-DOF
+    // tree keep nt = 3)
+    const bool big32 = !f64 && tiled && B >= kSeqMinBatch && mb->model.n <= 8;
+    const int pack = rbamd::tuning().pack >= 0 ? 0 : big32 ? 3 : B < kSeqMinBatch ? 1 : 0;
+    const int nt = (big32 && rbamd::tuning().rnea_nt < 0) ? 0 : -1;
     return jit_get(mb, rbamd::JitKind::Rnea, f64, fast, pack, rbamd::jit_seq_tail(tiled), nt);
 }
 

@@ -19,7 +19,9 @@ struct Tuning {
     // JIT fp32 forward dynamics / rollout lane form: 2 = two configurations per lane on packed
     // fp32 (spatial.hip.hpp f2; 512 configurations per 256-lane block), 1 = one per lane,
     // 4 = bias / mass-matrix split over a pair of packed waves, 5 = that split one per lane;
-    // -1 auto (capi.cpp jit_fd / launch_rollout_any by batch size, jit.cpp jit_pack).
+    // RNEA: 3 = two configurations per lane one after the other, 1 = one per lane;
+    // -1 auto (capi.cpp jit_rnea / jit_fd / launch_rollout_any by batch size and layout,
+    // jit.cpp jit_pack).
     std::atomic<int> pack{-1};
     // Precompiled (generic) RNEA launch form: 1 grid-stride + register prefetch, 0 one
     // configuration per lane, -1 auto (streaming for fp64 and chains longer than 8 links,
