@@ -507,13 +507,17 @@ RB_HD void sin_cos(f2 x, f2 &s, f2 &c) {
 
 // 1/x for the ABA's joint-space inertia D > 0 (normal range).  The IEEE division the
 // compiler emits is ~10 instructions (div_scale x2, rcp, 4 FMAs, div_fmas, div_fixup);
-// the hardware reciprocal is 1 ulp in fp32, and in fp64 two Newton steps on v_rcp_f64
-// land within 1 ulp as well.
+// the hardware reciprocal is 1 ulp in fp32.  In fp64 v_rcp_f64 is good to 4.6e-8 relative and
+// one Newton step to 2.2e-15 (~10 ulp; two steps: correctly rounded), measured over 2^22 inputs
+// across 2^-60..2^61 (tools/probe_rcp.hip, profiles/r04/ab/probe_rcp.log) -- far inside the
+// forward dynamics' 1e-8 tolerance, 14 VALU fewer per FR3 evaluation (jit_variant bit 1024 = the
+// second step, A/B only).
 __device__ __forceinline__ float recip(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ double recip(double x) {
     double r = __builtin_amdgcn_rcp(x);
     r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
-    return __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+    if constexpr ((RB_VARIANT & 1024) != 0) r = __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
+    return r;
 }
 __device__ __forceinline__ f2 recip(f2 x) { return f2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; }
 
