@@ -49,6 +49,10 @@ if __name__ == "__main__":
         # without non-temporal stores
         out = [run(7, ro, w, nt, B=B) for ro in (49, 42, 3) for (w, B) in ((2, 1 << 21), (1, 1 << 20))
                for nt in (0, 2, 3)]
+    elif len(sys.argv) > 1 and sys.argv[1] == "qtiled":
+        # CRBA / Jacobian fp64 shapes: SoA rows vs the tiled layout (nt bit 2), with / without
+        # non-temporal stores
+        out = [run(7, ro, 2, nt, B=1 << 21) for ro in (49, 42) for nt in (2, 4, 6, 7)]
     elif len(sys.argv) > 1 and sys.argv[1] == "chain30":
         # the 30-DOF RNEA shape (90 rows in / 30 out), SoA and tiled, with / without nt
         out = [run(90, 30, 1, nt, B=1 << 20) for nt in (0, 3, 4, 7)]
