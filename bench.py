@@ -353,9 +353,9 @@ def batch_launcher(mb, sets, kernel, dtype, layout="soa", B=None):
 Q_KERNELS = {"crba": lambda n: n * n, "jac": lambda n: 6 * n, "fwd_kin": lambda n: 3}
 
 
-def q_launcher(mb, kernel, B, dtype, rotate_gib, seed=chains.SEED):
-    """Closure issuing multibody_{crba,jac,fwd_kin}_batch_* on input set i % nsets (q only);
-    returns (launch, bytes per launch)."""
+def q_launcher(mb, kernel, B, dtype, rotate_gib, seed=chains.SEED, layout="soa"):
+    """Closure issuing multibody_{crba,jac,fwd_kin}_batch_* (or *_batch_tiled_*) on input set
+    i % nsets (q only); returns (launch, bytes per launch)."""
     n, rows = mb.n, Q_KERNELS[kernel](mb.n)
     es = 4 if dtype == torch.float32 else 8
     per = (n + rows) * B * es
@@ -365,11 +365,17 @@ def q_launcher(mb, kernel, B, dtype, rotate_gib, seed=chains.SEED):
     for s in range(ns):
         q = torch.empty((n, B), dtype=dtype, device="cuda")
         ffi.fill_uniform(q, lo, hi, seed + 1000 * s)
+        if layout == "tiled":
+            q = ffi.to_tiled(q)
+            outs.append(torch.empty((q.shape[0], rows, ffi.TILE), dtype=dtype, device="cuda"))
+        else:
+            outs.append(torch.empty((rows, B), dtype=dtype, device="cuda"))
         qs.append(q)
-        outs.append(torch.empty((rows, B), dtype=dtype, device="cuda"))
     torch.cuda.synchronize()
-    fn = getattr(ffi.lib(), f"multibody_{kernel}_batch_{'f32' if dtype == torch.float32 else 'f64'}")
-    calls = [(mb.handle, q.data_ptr(), o.data_ptr(), B, B) for q, o in zip(qs, outs)]
+    sfx = ("tiled_" if layout == "tiled" else "") + ("f32" if dtype == torch.float32 else "f64")
+    fn = getattr(ffi.lib(), f"multibody_{kernel}_batch_{sfx}")
+    tail = (B,) if layout == "tiled" else (B, B)
+    calls = [(mb.handle, q.data_ptr(), o.data_ptr()) + tail for q, o in zip(qs, outs)]
 
     def launch(i, sp):
         if fn(*calls[i % ns], sp):
@@ -524,17 +530,19 @@ def side_workloads(mb7, a):
     one("rnea_float14_tree_f32", mbt, "rnea", "f32")
     one("fd_float14_tree_f32", mbt, "fd", "f32")
     # batched mass matrix / Jacobian / forward kinematics: q in, n*n /
-    # 6n / 3 rows out per configuration, SoA, 2^20 configurations
+    # 6n / 3 rows out per configuration, SoA (fp64 also tiled), 2^20 configurations
     for kern in ("crba", "jac", "fwd_kin"):
-        for dn, dt in (("f64", torch.float64), ("f32", torch.float32)):
-            ql, per = q_launcher(mb7, kern, a.batch, dt, a.rotate_gib)
+        for dn, dt, lay in (("f64", torch.float64, "soa"), ("f64", torch.float64, "tiled"),
+                            ("f32", torch.float32, "soa")):
+            ql, per = q_launcher(mb7, kern, a.batch, dt, a.rotate_gib, layout=lay)
             nl = budget_steps(ql)
             w, km = time_launches(ql, nl, 3, 1, 100.0)
-            sec[f"{kern}_fr3_{dn}"] = {"evals_per_s": a.batch * nl / w, "kernel_ms_avg": km, "batch": a.batch,
-                                       "launches": nl, "layout": "soa", "dtype": dn,
-                                       "bytes_per_eval": per // a.batch,
-                                       "hbm_frac": per / (km * 1e-3) / HBM_PEAK,
-                                       "kernel_path": mb7.kernel_path(kern, dn == "f64", a.batch)}
+            name = f"{kern}_fr3_{dn}" + ("_tiled" if lay == "tiled" else "")
+            sec[name] = {"evals_per_s": a.batch * nl / w, "kernel_ms_avg": km, "batch": a.batch,
+                         "launches": nl, "layout": lay, "dtype": dn,
+                         "bytes_per_eval": per // a.batch,
+                         "hbm_frac": per / (km * 1e-3) / HBM_PEAK,
+                         "kernel_path": mb7.kernel_path(kern, dn == "f64", a.batch)}
             del ql
     torch.cuda.empty_cache()
     # fused rollout: K forward-dynamics + Euler steps per launch

@@ -203,6 +203,17 @@ int multibody_fwd_kin_batch_f32(const Multibody *mb, const float *q, float *pos,
                                 int64_t batch, int64_t ld, void *stream);
 int multibody_jac_batch_f32(const Multibody *mb, const float *q, float *J,
                             int64_t batch, int64_t ld, void *stream);
+/* The q-only queries on the tiled layout: q is [ceil(batch/256)][n][256], the output
+ * [ceil(batch/256)][rows][256] with rows = n*n (crba), 6n (jac), 3 (fwd_kin), elements in the
+ * same order as the SoA rows above.  Bit-identical to the SoA forms. */
+int multibody_crba_batch_tiled_f32(const Multibody *mb, const float *q, float *H, int64_t batch, void *stream);
+int multibody_crba_batch_tiled_f64(const Multibody *mb, const double *q, double *H, int64_t batch, void *stream);
+int multibody_fwd_kin_batch_tiled_f32(const Multibody *mb, const float *q, float *pos, int64_t batch,
+                                      void *stream);
+int multibody_fwd_kin_batch_tiled_f64(const Multibody *mb, const double *q, double *pos, int64_t batch,
+                                      void *stream);
+int multibody_jac_batch_tiled_f32(const Multibody *mb, const float *q, float *J, int64_t batch, void *stream);
+int multibody_jac_batch_tiled_f64(const Multibody *mb, const double *q, double *J, int64_t batch, void *stream);
 
 /* ---- batched host-pointer entry points (blocking) ------------------------------ */
 int multibody_rnea_batch_host_f64(const Multibody *mb, const double *q, const double *qd,

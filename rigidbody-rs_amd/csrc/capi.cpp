@@ -353,14 +353,16 @@ hipError_t launch_rollout_any(const Multibody *mb, const T *mdl, T *q, T *qd, co
 
 template <typename T>
 hipError_t launch_crba_any(const Multibody *mb, const T *mdl, const T *q, T *H, uint32_t B, int64_t ld,
-                           hipStream_t s) {
+                           hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
     if (const rbamd::JitKernel *jk = jit_get(mb, rbamd::JitKind::Crba, sizeof(T) == 8, false)) {
-        void *args[] = {(void *)&q, (void *)&H, (void *)&B, (void *)&ld};
+        const int64_t n = mb->model.n, lda = tiled ? 256 : ld, bs_in = tiled ? n * 256 : 256,
+                      bs_out = tiled ? n * n * 256 : 256;
+        void *args[] = {(void *)&q, (void *)&H, (void *)&B, (void *)&lda, (void *)&bs_in, (void *)&bs_out};
         return jit_launch(jk, B, args, s);
     }
     if (!mb->model.serial_revolute()) return no_generic(mb);
-    return rbamd::launch_crba<T>(mb->model.n, mdl, q, H, B, ld, s);
+    return rbamd::launch_crba<T>(mb->model.n, mdl, q, H, B, ld, s, tiled);
 }
 
 // fwd_kin / jac: the hipRTC kernels (tree_body.hip.hpp fwd_kin_tree / jac_tree, the model's
@@ -381,15 +383,17 @@ bool kin_precompiled(const Multibody *mb) {
 
 template <typename T>
 hipError_t launch_kin_any(const Multibody *mb, bool jac, const T *mdl, const T *q, T *out, uint32_t B, int64_t ld,
-                          hipStream_t s) {
+                          hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
     const bool fast = sizeof(T) == 4 && fast_trig();
     const rbamd::JitKernel *jk = kin_precompiled(mb) ? nullptr : jit_kin(mb, jac, sizeof(T) == 8);
     if (!jk && mb->model.serial_revolute())
-        return jac ? rbamd::launch_jac<T>(mb->model.n, mdl, q, out, B, ld, s, fast)
-                   : rbamd::launch_fwd_kin<T>(mb->model.n, mdl, q, out, B, ld, s, fast);
+        return jac ? rbamd::launch_jac<T>(mb->model.n, mdl, q, out, B, ld, s, fast, tiled)
+                   : rbamd::launch_fwd_kin<T>(mb->model.n, mdl, q, out, B, ld, s, fast, tiled);
     if (!jk) return no_generic(mb);
-    void *args[] = {(void *)&q, (void *)&out, (void *)&B, (void *)&ld};
+    const int64_t n = mb->model.n, lda = tiled ? 256 : ld, bs_in = tiled ? n * 256 : 256,
+                  bs_out = tiled ? (jac ? 6 * n : 3) * 256 : 256;
+    void *args[] = {(void *)&q, (void *)&out, (void *)&B, (void *)&lda, (void *)&bs_in, (void *)&bs_out};
     return jit_launch(jk, B, args, s);
 }
 
@@ -545,29 +549,33 @@ int rollout_batch(const Multibody *mb, T *q, T *qd, const T *tau_seq, double dt,
 }
 
 template <typename T>
-int crba_batch(const Multibody *mb, const T *q, T *H, int64_t batch, int64_t ld, void *stream) {
-    int rc = check_batch(mb, batch, ld);
+int crba_batch(const Multibody *mb, const T *q, T *H, int64_t batch, int64_t ld, void *stream, bool tiled = false) {
+    int rc = check_batch(mb, batch, tiled ? batch : ld);
     if (rc) return rc;
     if (batch == 0) return RB_OK;
     if (!q || !H) return set_err(RB_ERR_NULL, "NULL array");
     const T *mdl = nullptr;
     if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    // element offsets of configuration b0 (b0 % 256 == 0) in the input / output arrays
+    const int64_t n = mb->model.n, pin = tiled ? n : 1, pout = tiled ? n * n : 1;
     return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = launch_crba_any<T>(mb, mdl, q + b0, H + b0, nb, ld, (hipStream_t)stream);
+        hipError_t e = launch_crba_any<T>(mb, mdl, q + b0 * pin, H + b0 * pout, nb, ld, (hipStream_t)stream, tiled);
         return e == hipSuccess ? RB_OK : hip_err(e, "crba launch");
     });
 }
 
 template <typename T>
-int kin_batch(const Multibody *mb, bool jac, const T *q, T *out, int64_t batch, int64_t ld, void *stream) {
-    int rc = check_batch(mb, batch, ld);
+int kin_batch(const Multibody *mb, bool jac, const T *q, T *out, int64_t batch, int64_t ld, void *stream,
+              bool tiled = false) {
+    int rc = check_batch(mb, batch, tiled ? batch : ld);
     if (rc) return rc;
     if (batch == 0) return RB_OK;
     if (!q || !out) return set_err(RB_ERR_NULL, "NULL array");
     const T *mdl = nullptr;
     if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    const int64_t n = mb->model.n, pin = tiled ? n : 1, pout = tiled ? (jac ? 6 * n : 3) : 1;
     return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
-        hipError_t e = launch_kin_any<T>(mb, jac, mdl, q + b0, out + b0, nb, ld, (hipStream_t)stream);
+        hipError_t e = launch_kin_any<T>(mb, jac, mdl, q + b0 * pin, out + b0 * pout, nb, ld, (hipStream_t)stream, tiled);
         return e == hipSuccess ? RB_OK : hip_err(e, jac ? "jac launch" : "fwd_kin launch");
     });
 }
@@ -1016,6 +1024,26 @@ int multibody_crba_batch_f32(const Multibody *mb, const float *q, float *H, int6
 int multibody_crba_batch_f64(const Multibody *mb, const double *q, double *H, int64_t batch, int64_t ld,
                              void *stream) {
     return crba_batch<double>(mb, q, H, batch, ld, stream);
+}
+
+int multibody_crba_batch_tiled_f32(const Multibody *mb, const float *q, float *H, int64_t batch, void *stream) {
+    return crba_batch<float>(mb, q, H, batch, 256, stream, true);
+}
+int multibody_crba_batch_tiled_f64(const Multibody *mb, const double *q, double *H, int64_t batch, void *stream) {
+    return crba_batch<double>(mb, q, H, batch, 256, stream, true);
+}
+int multibody_fwd_kin_batch_tiled_f32(const Multibody *mb, const float *q, float *pos, int64_t batch, void *stream) {
+    return kin_batch<float>(mb, false, q, pos, batch, 256, stream, true);
+}
+int multibody_fwd_kin_batch_tiled_f64(const Multibody *mb, const double *q, double *pos, int64_t batch,
+                                      void *stream) {
+    return kin_batch<double>(mb, false, q, pos, batch, 256, stream, true);
+}
+int multibody_jac_batch_tiled_f32(const Multibody *mb, const float *q, float *J, int64_t batch, void *stream) {
+    return kin_batch<float>(mb, true, q, J, batch, 256, stream, true);
+}
+int multibody_jac_batch_tiled_f64(const Multibody *mb, const double *q, double *J, int64_t batch, void *stream) {
+    return kin_batch<double>(mb, true, q, J, batch, 256, stream, true);
 }
 
 int multibody_fwd_kin_batch_f64(const Multibody *mb, const double *q, double *pos, int64_t batch,

@@ -371,16 +371,21 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << "  if (b >= B) return;\n";
         o << "  rbamd::dev::rollout_lane<T, N, " << F << ", Topo>(kModel, q, qd, tau_seq, dt, K, traj, b, ld, sh);\n}\n";
     } else if (kind == JitKind::FwdKin || kind == JitKind::Jac) {
-        o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ out, uint32_t B, int64_t ld) {\n";
+        // q-only kernels take the block strides of their input and output rows (256 for SoA;
+        // n * 256 / rows * 256 for the tiled layout), as the lane kernels above
+        o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ out, uint32_t B, int64_t ld, "
+             "int64_t bs_in, int64_t bs_out) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
         o << "  rbamd::dev::" << (kind == JitKind::FwdKin ? "fwd_kin" : "jac") << "_lane_tree<T, N, " << F
-          << ", Topo>(kModel, q, out, b, ld);\n}\n";
+          << ", Topo>(kModel, q + (int64_t)blockIdx.x * bs_in, out + (int64_t)blockIdx.x * bs_out, threadIdx.x, ld);\n}\n";
     } else {
-        o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ H, uint32_t B, int64_t ld) {\n";
+        o << head << "rb_jit_kernel(const T *__restrict__ q, T *__restrict__ H, uint32_t B, int64_t ld, "
+             "int64_t bs_in, int64_t bs_out) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
         o << "  if (b >= B) return;\n";
-        o << "  rbamd::dev::crba_lane<T, N, " << F << ", Topo>(kModel, q, H, b, ld);\n}\n";
+        o << "  rbamd::dev::crba_lane<T, N, " << F
+          << ", Topo>(kModel, q + (int64_t)blockIdx.x * bs_in, H + (int64_t)blockIdx.x * bs_out, threadIdx.x, ld);\n}\n";
     }
     std::string src = o.str();
     if (tab) {  // every kernel fills the block's sincos table first (all lanes still present)

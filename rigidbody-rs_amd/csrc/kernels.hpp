@@ -45,13 +45,13 @@ hipError_t launch_rollout(int n, const T *mdl, T *q, T *qd, const T *tau_seq, T 
                           int64_t ld, hipStream_t s, bool fast);
 template <typename T>
 hipError_t launch_crba(int n, const T *mdl, const T *q, T *H, uint32_t B, int64_t ld,
-                       hipStream_t s);
+                       hipStream_t s, bool tiled = false);
 template <typename T>
 hipError_t launch_fwd_kin(int n, const T *mdl, const T *q, T *pos, uint32_t B, int64_t ld,
-                          hipStream_t s, bool fast);
+                          hipStream_t s, bool fast, bool tiled = false);
 template <typename T>
 hipError_t launch_jac(int n, const T *mdl, const T *q, T *J, uint32_t B, int64_t ld,
-                      hipStream_t s, bool fast);
+                      hipStream_t s, bool fast, bool tiled = false);
 template <typename T>
 hipError_t launch_fill_uniform(T *x, int rows, uint32_t B, int64_t ld, const double *lohi_dev,
                                uint64_t seed, hipStream_t s);

@@ -16,12 +16,14 @@ template <typename T, int N, bool FAST>
 __global__ __launch_bounds__(kBlock) void fwd_kin_kernel(const T *__restrict__ gmdl,
                                                          const T *__restrict__ q,
                                                          T *__restrict__ pos, uint32_t B,
-                                                         int64_t ld) {
+                                                         int64_t ld, int64_t bs_in, int64_t bs_out) {
     __shared__ T mdl[N * kLinkStride];
     stage_model<T, N, kBlock>(gmdl, mdl);
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= B) return;
-    const uint32_t off = b * (uint32_t)sizeof(T);
+    q += (int64_t)blockIdx.x * bs_in;  // block k's rows (crba.hip)
+    pos += (int64_t)blockIdx.x * bs_out;
+    const uint32_t off = threadIdx.x * (uint32_t)sizeof(T);
     // T_0 T_1 ... T_{n-1} accumulated from the base: p += R p_i, R = R E_i
     M3<T> R{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
     V3<T> p = v3(T(0), T(0), T(0));
@@ -49,12 +51,14 @@ template <typename T, int N, bool FAST>
 __global__ __launch_bounds__(kBlock) void jac_kernel(const T *__restrict__ gmdl,
                                                      const T *__restrict__ q,
                                                      T *__restrict__ J, uint32_t B,
-                                                     int64_t ld) {
+                                                     int64_t ld, int64_t bs_in, int64_t bs_out) {
     __shared__ T mdl[N * kLinkStride];
     stage_model<T, N, kBlock>(gmdl, mdl);
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= B) return;
-    const uint32_t off = b * (uint32_t)sizeof(T);
+    q += (int64_t)blockIdx.x * bs_in;
+    J += (int64_t)blockIdx.x * bs_out;
+    const uint32_t off = threadIdx.x * (uint32_t)sizeof(T);
     // acc = pose of the last frame in frame i, built leaf -> root (multibody.rs:97-106):
     // column i = motion transform of S_i = (0,0,1 | 0) by acc:
     //   rot = R^T z,  lin = R^T (0 - p x z) = -R^T (p.y, -p.x, 0)
@@ -149,16 +153,18 @@ __global__ __launch_bounds__(kBlock) void fill_uniform_kernel(T *__restrict__ x,
 
 template <typename T>
 hipError_t launch_fwd_kin(int n, const T *mdl, const T *q, T *pos, uint32_t B, int64_t ld,
-                          hipStream_t s, bool fast) {
+                          hipStream_t s, bool fast, bool tiled) {
     if (B == 0) return hipSuccess;
     const dim3 grid(dev::grid_for(B)), block(dev::kBlock);
+    const int64_t lda = tiled ? dev::kBlock : ld, bs_in = tiled ? (int64_t)n * dev::kBlock : dev::kBlock,
+                  bs_out = tiled ? 3 * dev::kBlock : dev::kBlock;
     switch (n) {
 #define RB_CASE(N)                                                                              \
     case N:                                                                                     \
         if (fast)                                                                               \
-            hipLaunchKernelGGL((dev::fwd_kin_kernel<T, N, true>), grid, block, 0, s, mdl, q, pos, B, ld); \
+            hipLaunchKernelGGL((dev::fwd_kin_kernel<T, N, true>), grid, block, 0, s, mdl, q, pos, B, lda, bs_in, bs_out); \
         else                                                                                    \
-            hipLaunchKernelGGL((dev::fwd_kin_kernel<T, N, false>), grid, block, 0, s, mdl, q, pos, B, ld); \
+            hipLaunchKernelGGL((dev::fwd_kin_kernel<T, N, false>), grid, block, 0, s, mdl, q, pos, B, lda, bs_in, bs_out); \
         break;
         RB_FOR_EACH_DOF(RB_CASE)
 #undef RB_CASE
@@ -170,16 +176,18 @@ hipError_t launch_fwd_kin(int n, const T *mdl, const T *q, T *pos, uint32_t B, i
 
 template <typename T>
 hipError_t launch_jac(int n, const T *mdl, const T *q, T *J, uint32_t B, int64_t ld,
-                      hipStream_t s, bool fast) {
+                      hipStream_t s, bool fast, bool tiled) {
     if (B == 0) return hipSuccess;
     const dim3 grid(dev::grid_for(B)), block(dev::kBlock);
+    const int64_t lda = tiled ? dev::kBlock : ld, bs_in = tiled ? (int64_t)n * dev::kBlock : dev::kBlock,
+                  bs_out = tiled ? 6 * (int64_t)n * dev::kBlock : dev::kBlock;
     switch (n) {
 #define RB_CASE(N)                                                                              \
     case N:                                                                                     \
         if (fast)                                                                               \
-            hipLaunchKernelGGL((dev::jac_kernel<T, N, true>), grid, block, 0, s, mdl, q, J, B, ld); \
+            hipLaunchKernelGGL((dev::jac_kernel<T, N, true>), grid, block, 0, s, mdl, q, J, B, lda, bs_in, bs_out); \
         else                                                                                    \
-            hipLaunchKernelGGL((dev::jac_kernel<T, N, false>), grid, block, 0, s, mdl, q, J, B, ld); \
+            hipLaunchKernelGGL((dev::jac_kernel<T, N, false>), grid, block, 0, s, mdl, q, J, B, lda, bs_in, bs_out); \
         break;
         RB_FOR_EACH_DOF(RB_CASE)
 #undef RB_CASE
@@ -219,12 +227,12 @@ template hipError_t launch_to_tiled<double>(const double *, int64_t, double *, i
 template hipError_t launch_from_tiled<float>(const float *, float *, int64_t, int, uint32_t, hipStream_t);
 template hipError_t launch_from_tiled<double>(const double *, double *, int64_t, int, uint32_t, hipStream_t);
 template hipError_t launch_fwd_kin<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t,
-                                           bool);
+                                           bool, bool);
 template hipError_t launch_jac<double>(int, const double *, const double *, double *, uint32_t, int64_t, hipStream_t,
-                                       bool);
+                                       bool, bool);
 template hipError_t launch_fwd_kin<float>(int, const float *, const float *, float *, uint32_t, int64_t, hipStream_t,
-                                          bool);
-template hipError_t launch_jac<float>(int, const float *, const float *, float *, uint32_t, int64_t, hipStream_t, bool);
+                                          bool, bool);
+template hipError_t launch_jac<float>(int, const float *, const float *, float *, uint32_t, int64_t, hipStream_t, bool, bool);
 template hipError_t launch_fill_uniform<float>(float *, int, uint32_t, int64_t, const double *, uint64_t, hipStream_t);
 template hipError_t launch_fill_uniform<double>(double *, int, uint32_t, int64_t, const double *, uint64_t, hipStream_t);
 

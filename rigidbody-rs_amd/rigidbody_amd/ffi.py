@@ -106,6 +106,8 @@ for _t in ("f32", "f64"):
     _sig(f"multibody_rnea_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp])
     _sig(f"multibody_fd_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp])
     _sig(f"rb_to_tiled_{_t}", ctypes.c_int, [_vp, _i64, _vp, ctypes.c_int, _i64, _vp])
+    for _k in ("crba", "fwd_kin", "jac"):
+        _sig(f"multibody_{_k}_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _i64, _vp])
     _sig(f"rb_from_tiled_{_t}", ctypes.c_int, [_vp, _vp, _i64, ctypes.c_int, _i64, _vp])
 TILE = 256  # configurations per tile of the tiled layout (rigidbody_batch.h)
 
@@ -434,6 +436,31 @@ class Multibody:
 
     def fd_batch_tiled(self, q, qd, tau, B, out=None, stream=None):
         return self._tiled_call("fd", q, qd, tau, B, out, stream)
+
+    def _q_tiled(self, kind, rows, q, B, out, stream):
+        q = self._tiled(q, "q", B)
+        if q.dtype not in (torch.float32, torch.float64):
+            raise TypeError(f"q has dtype {q.dtype}, expected float32 or float64")
+        shape = ((B + TILE - 1) // TILE, rows, TILE)
+        if out is None:
+            out = torch.empty(shape, dtype=q.dtype, device=q.device)
+        elif tuple(out.shape) != shape or out.dtype != q.dtype or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous {list(shape)} tensor of q's dtype")
+        dev = _one_device((q, out))
+        fn = getattr(_lib, f"multibody_{kind}_batch_tiled_{_TORCH_SUFFIX[q.dtype]}")
+        with torch.cuda.device(dev):
+            _check(fn(self._h, q.data_ptr(), out.data_ptr(), B, _stream_ptr(stream, dev)), f"{kind}_batch_tiled")
+        return out
+
+    def crba_batch_tiled(self, q, B, out=None, stream=None):
+        """Mass matrices on the tiled layout: q [ceil(B/256), n, 256] -> [ceil(B/256), n*n, 256]."""
+        return self._q_tiled("crba", self.n * self.n, q, B, out, stream)
+
+    def fwd_kin_batch_tiled(self, q, B, out=None, stream=None):
+        return self._q_tiled("fwd_kin", 3, q, B, out, stream)
+
+    def jac_batch_tiled(self, q, B, out=None, stream=None):
+        return self._q_tiled("jac", 6 * self.n, q, B, out, stream)
 
     def rollout_batch(self, q, qd, tau_seq, dt, traj=False, stream=None):
         """K fused forward-dynamics + semi-implicit Euler steps, in place on q and qd

@@ -571,7 +571,8 @@ def test_paired_rollout_vs_single_and_oracle(B, ffi, dev, fr3_text):
 def test_tiled_layout_matches_soa_bitwise(name, ffi, dev, fr3_text):
     """The tiled [ceil(B/256), n, 256] entry points run the same lane arithmetic as the
     SoA ones: outputs are bit-identical (JIT and generic kernels, fp32 and fp64, ragged
-    batches), the layout conversions are exact round trips, and the oracle agrees.  From 2^19
+    batches; RNEA, forward dynamics, CRBA, fwd_kin and jac), the layout conversions are exact
+    round trips, and the oracle agrees.  From 2^19
     the fp32 FR3 tiled launch compiles without non-temporal loads / stores (tuning rnea_nt auto)
     while the SoA launch keeps them: still the same arithmetic, bit for bit."""
     mb = ffi.Multibody.from_urdf_string(_model_xml(name, fr3_text))
@@ -593,6 +594,11 @@ def test_tiled_layout_matches_soa_bitwise(name, ffi, dev, fr3_text):
                     qdd2 = mb.fd_batch(x[0], x[1], tau)
                     qdd2_t = ffi.from_tiled(mb.fd_batch_tiled(xt[0], xt[1], ffi.to_tiled(tau), B), B)
                     assert torch.equal(qdd2, qdd2_t), (jit, B, dt)
+                    # the q-only queries on the same tiles
+                    for kind in ("crba", "fwd_kin", "jac"):
+                        soa = getattr(mb, f"{kind}_batch")(x[0])
+                        til = ffi.from_tiled(getattr(mb, f"{kind}_batch_tiled")(xt[0], B), B)
+                        assert torch.equal(soa, til), (kind, jit, B, dt)
                     if dt == torch.float64 and B <= 1000:
                         _close(tau_t.cpu().numpy(), om.rnea_batch(q, qd, qdd), 1e-9, f"tiled rnea B={B}")
                         _close(qdd2_t.cpu().numpy(), qdd, 1e-7, f"tiled fd round trip B={B}")

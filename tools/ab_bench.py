@@ -49,8 +49,8 @@ def main():
     for lay in a.layouts:
         if a.kernel == "rollout":
             launches[lay] = bench.rollout_launcher(mb, a.batch, dtype, a.rollout_k)
-        elif a.kernel in bench.Q_KERNELS:  # crba / jac / fwd_kin: q in, SoA only
-            launches[lay] = bench.q_launcher(mb, a.kernel, a.batch, dtype, 1.25)[0]
+        elif a.kernel in bench.Q_KERNELS:  # crba / jac / fwd_kin: q in
+            launches[lay] = bench.q_launcher(mb, a.kernel, a.batch, dtype, 1.25, layout=lay)[0]
         else:
             sets = bench.make_sets(mb, a.batch, dtype, a.kernel, nsets, chains.SEED, lay)
             launches[lay] = bench.batch_launcher(mb, sets, a.kernel, dtype, lay, a.batch)
