@@ -164,6 +164,16 @@ def test_null_handle_paths_do_not_abort(ffi):
     lib.multibody_free(None)
     assert lib.multibody_rnea_batch_f32(None, None, None, None, None, 0, 0, None) == 1
     assert "NULL" in ffi.last_error()
+    # the tiled q-only entry points: NULL handle, then NULL arrays with a live handle, refused
+    # before any device work (no GPU here)
+    mb = ffi.Multibody.new()
+    for k in ("crba", "fwd_kin", "jac"):
+        for t in ("f32", "f64"):
+            fn = getattr(lib, f"multibody_{k}_batch_tiled_{t}")
+            assert fn(None, None, None, 1, None) == 1, (k, t)
+            assert fn(mb.handle, None, None, 1, None) == 1, (k, t)
+            assert "NULL" in ffi.last_error()
+            assert fn(mb.handle, None, None, 0, None) == 0, (k, t)  # empty batch: nothing to do
 
 
 def test_index_pairing_detected(ffi):

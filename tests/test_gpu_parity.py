@@ -604,6 +604,8 @@ def test_tiled_layout_matches_soa_bitwise(name, ffi, dev, fr3_text):
                         _close(qdd2_t.cpu().numpy(), qdd, 1e-7, f"tiled fd round trip B={B}")
         with pytest.raises(ValueError):
             mb.rnea_batch_tiled(xt[0][:, :, :128].contiguous(), xt[1], xt[2], 65536 + 3)
+        with pytest.raises(ValueError):  # an [tiles, n, 256] array is not a Jacobian's [tiles, 6n, 256]
+            mb.jac_batch_tiled(xt[0], (1 << 19) + 5, out=xt[1])
     finally:
         ffi.set_tuning("jit", 1)
 
