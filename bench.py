@@ -497,6 +497,9 @@ def side_workloads(mb7, a):
                 sec[name]["valu"] = valu_roofline(workload_name(kernel, mb.n, dt_name, layout, B), f"{kernel}_{model}",
                                                   f"{kernel}_{model}_{dt_name}" + ("" if B == a.batch else f"_b{B}"),
                                                   dt_name, B, r["kernel_ms_avg"], form in (2, 4))
+                ref = reference_formulation(f"{kernel}_{model}", B, r["kernel_ms_avg"])
+                if ref:
+                    sec[name]["reference_formulation"] = ref
         if graph:  # the same launches replayed from a HIP graph; rates over the launches replayed
             gl = r["graph_launches"]
             # eager back-to-back launches from Python are host-bound when the graph replay of the
@@ -556,7 +559,8 @@ def side_workloads(mb7, a):
                                         "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", dn == "f64"),
                                         "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)",
                                         "valu": valu_roofline(f"rollout_fr3_{dn}_K16_b{a.batch}", "rollout_step_fr3",
-                                                              f"rollout_fr3_{dn}", dn, a.batch * K, km, dn == "f32")}
+                                                              f"rollout_fr3_{dn}", dn, a.batch * K, km, dn == "f32"),
+                                        "reference_formulation": reference_formulation("rollout_step_fr3", a.batch * K, km)}
     # the MPC-sized rollout (65536 configurations, K = 16): the split of packed waves per step
     # (rollout_split_block2), device-bound rate from a HIP graph
     Bs = 65536
@@ -734,17 +738,13 @@ def valu_roofline(workload, op_key, clock_key, dt_name, evals, kern_ms, packed):
         MI355X_MICROARCH.md 'Per-instruction cycle constants').
       flop_frac = VALU FLOPs executed (gfx950 SQ_INSTS_VALU_FLOPS_*, x 64 lanes) / the dtype's
         vector peak (fp32 157.3 TF, fp64 78.6 TF at 2.4 GHz).
-      flops_per_eval_ref = the reference formulation's operations per evaluation (op-counting
-        oracle build, profiles/r04/op_counts.json) -- what the kernel replaces, not what it runs."""
+    Every figure here is what the kernel itself executes, so each *_frac is <= 1 and no rate
+    exceeds its peak (roofline_violations); the reference formulation's operation count is
+    reported beside the roofline, not in it (reference_formulation)."""
     tr = load_traffic(workload)
-    ops = _load_json("profiles/r04/op_counts.json")
     t = kern_ms * 1e-3
     cyc = 4 if (dt_name == "f64" or packed) else 2
     out = {"bound": "valu", "unit": "fraction", "evals_per_launch": evals, "cycles_per_valu_inst": cyc}
-    if ops and op_key in ops:
-        ref = ops[op_key]["flops"]
-        out.update({"flops_per_eval_ref": ref, "ref_equiv_tflops": ref * evals / t / 1e12,
-                    "ref_source": f"profiles/r04/op_counts.json [{op_key}] (oracle/flops.cpp)"})
     sq = (tr or {}).get("sq_counters_per_launch", {})
     if "SQ_INSTS_VALU" in sq:
         busy = sq["SQ_INSTS_VALU"] * cyc / SIMDS  # vector issue cycles per SIMD per launch
@@ -767,6 +767,62 @@ def valu_roofline(workload, op_key, clock_key, dt_name, evals, kern_ms, packed):
                         "flop_frac": kf / t / VALU_FLOP_PEAK[dt_name], "flop_peak_tflops": VALU_FLOP_PEAK[dt_name] / 1e12})
         out["counters_source"] = f"profiles/traffic_{workload}.json (rocprofv3 PMC passes of this kernel)"
     return out
+
+
+CONFIG4_BATCH = 1 << 20  # the global fp64 RNEA + FD batch
+
+
+def reference_formulation(op_key, evals, kern_ms):
+    """The reference formulation's operations per evaluation (op-counting build of the oracle,
+    oracle/flops.cpp -> profiles/r04/op_counts.json: quaternion transforms, isometry inverses,
+    6-vector cross products as multibody.rs / spatial.rs / inertia.rs write them) and the FLOP
+    rate that formulation would need to match this kernel's evaluation rate.  Not a roofline
+    figure: the kernel executes 2.7-4.4x fewer operations (roofline.valu.kernel_flops_per_eval),
+    so this rate may exceed the VALU peak."""
+    ops = _load_json("profiles/r04/op_counts.json")
+    if not ops or op_key not in ops or not kern_ms:
+        return None
+    ref = ops[op_key]["flops"]
+    return {"flops_per_eval": ref, "equiv_tflops_at_this_rate": ref * evals / (kern_ms * 1e-3) / 1e12,
+            "source": f"profiles/r04/op_counts.json [{op_key}] (oracle/flops.cpp)",
+            "note": "what the reference's formulation would have to execute per second for this "
+                    "evaluation rate; not a roofline figure (the kernel runs fewer operations)"}
+
+
+def roofline_violations(line):
+    """Consistency of a bench line's roofline block (tests/test_bench_launch.py): every *_frac
+    anywhere in the line within (0, 1], roofline.achieved <= roofline.peak, and the VALU block's
+    kernel_tflops <= flop_peak_tflops.  Returns the list of violations (empty = consistent)."""
+    bad = []
+
+    def walk(x, path):
+        if isinstance(x, dict):
+            for k, v in x.items():
+                p = f"{path}.{k}" if path else k
+                if k.endswith("frac") and isinstance(v, (int, float)) and not (0 < v <= 1.0):
+                    bad.append(f"{p} = {v}")
+                walk(v, p)
+        elif isinstance(x, list):
+            for i, v in enumerate(x):
+                walk(v, f"{path}[{i}]")
+
+    walk(line, "")
+    rf = line.get("roofline") or {}
+    if rf.get("achieved") is not None and rf.get("peak") and rf["achieved"] > rf["peak"]:
+        bad.append(f"roofline.achieved {rf['achieved']} > peak {rf['peak']}")
+
+    def valu_rates(x, path):
+        if isinstance(x, dict):
+            if "kernel_tflops" in x and "flop_peak_tflops" in x and x["kernel_tflops"] > x["flop_peak_tflops"]:
+                bad.append(f"{path}.kernel_tflops {x['kernel_tflops']} > {x['flop_peak_tflops']}")
+            for k, v in x.items():
+                valu_rates(v, f"{path}.{k}")
+
+    valu_rates(rf, "roofline")
+    for k, v in (line.get("secondary") or {}).items():
+        if isinstance(v, dict) and isinstance(v.get("valu"), dict):
+            valu_rates(v["valu"], f"secondary.{k}.valu")
+    return bad
 
 
 def workload_name(kernel, n, dt_name, layout, B):
@@ -841,6 +897,9 @@ def main(a):
         form = mb.kernel_form(a.kernel.split("_")[0], a.dtype == "f64", B, a.layout == "tiled")
         line["roofline"]["valu"] = valu_roofline(workload, f"{a.kernel.split('_')[0]}_{model}",
                                                  f"{a.kernel}_{model}_{a.dtype}", a.dtype, B, kern_ms, form in (2, 4))
+        ref = reference_formulation(f"{a.kernel.split('_')[0]}_{model}", B, kern_ms)
+        if ref:
+            line["reference_formulation"] = ref
     if world > 1:
         line["per_rank"] = ranks
     sec = {}
@@ -861,6 +920,31 @@ def main(a):
                                "ms_per_step": sw / rs["steps"] * 1e3, "kernel_ms_avg_max_rank": sk,
                                "per_rank": per_rank(rs, world, dev), "scaling": "strong",
                                "timing": "own launch budget (bench.budget_steps, max over ranks), not --steps"}
+        # SURVEY §8(d) config 4 -- "fr3 RNEA+ABA batch=2^20 fp64, sharded across 8 x MI355X": every
+        # rank runs multibody_rnea_batch_f64 then multibody_fd_batch_f64 on its contiguous shard of
+        # one global 2^20 batch (2^17 per GPU at N = 8; multibody.rs:111-174), own launch budget
+        cfg4 = CONFIG4_BATCH
+        c4lo, c4hi = rdist.shard(cfg4, rank, world)
+        if a.stub:
+            r4 = stub_measure(c4hi - c4lo, SIDE_MIN_LAUNCHES)
+            k4 = "stub"
+        else:
+            r4 = measure(mb, "rnea_fd", "f64", c4hi - c4lo, a.layout, None, 5, world, a.rotate_gib, chains.SEED,
+                         100.0, dev=dev)
+            k4 = "+".join(mb.kernel_path(k, True, c4hi - c4lo, a.layout == "tiled") for k in ("rnea", "fd"))
+        w4, km4 = rdist.max_over_ranks([r4["wall"], r4["kernel_ms_avg"]], world, dev)
+        b4 = set_bytes(n, 1, 8, "rnea_fd")
+        sec["strong_split_rnea_fd"] = {
+            "config": "SURVEY §8(d) config 4: fr3 RNEA + forward dynamics, fp64, one global batch of "
+                      f"{cfg4} sharded across {world} GPUs (contiguous shards, no collective on the data path)",
+            "pairs_per_s": cfg4 * r4["steps"] / w4, "global_batch": cfg4, "batch_per_gpu_max": -(-cfg4 // world),
+            "launches": r4["steps"], "ms_per_step": w4 / r4["steps"] * 1e3, "kernel_ms_avg_max_rank": km4,
+            "hbm_frac_max_rank": b4 * -(-cfg4 // world) / (km4 * 1e-3) / HBM_PEAK if not a.stub else None,
+            "bytes_per_pair": b4, "kernel_path": k4, "dtype": "f64", "layout": a.layout,
+            "per_rank": per_rank(r4, world, dev), "scaling": "strong",
+            "timing": "own launch budget (bench.budget_steps; one step = the RNEA launch + the FD launch on "
+                      "the rank's shard), max over ranks",
+            "status": "measured by the driver's N > 1 runs; our 1-GPU leases cannot run it (DESIGN.md §6)"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.stub:
         line["cpu_baseline"] = cpu_baseline(n, a.kernel, a.cpu_seconds)
     elif world > 1:
@@ -884,6 +968,8 @@ def main(a):
                                                              "crba": cb["single_thread_crba_us_per_call"]}
     if sec:
         line["secondary"] = sec
+    viol = roofline_violations(line)
+    line["roofline_check"] = "ok" if not viol else viol  # fractions <= 1, rates <= peak
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

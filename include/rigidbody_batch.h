@@ -34,6 +34,23 @@
  * Reentrancy: a Multibody is immutable after construction; calls on one handle
  * from several threads are safe (device model constants are uploaded once per
  * device under a lock; the single-config ABI uses thread-local staging).
+ *
+ * Input domain.  The reference evaluates any f64 joint angle exactly (libm sin/cos in
+ * UnitQuaternion::from_scaled_axis, joint.rs:48-50) and lets NaN / Inf flow through its
+ * arithmetic.  The batched kernels are exact (at the |q| <= pi tolerances of the tests) for
+ *   every input finite (|x| < 2^1017 in fp64) and every revolute angle |q_j| < 2^41 rad
+ *   (fp64) / 2^22 rad (fp32)
+ * -- each sincos reduces the angle exactly over that range (spatial.hip.hpp; tested at
+ * |q| up to 1e6 rad, tests/test_gpu_domain.py).  A configuration outside it -- a NaN or
+ * +-Inf in any of its inputs, or an angle past the bound -- gets NaN in EVERY output (CRBA:
+ * every upper-triangle entry; the strictly-lower entries stay the ABI's exact zeros), in
+ * every kernel form; the other configurations of the batch, including the other half of a
+ * paired lane, are unaffected.  Rollouts check the state and tau_k every step: a trajectory
+ * is NaN from the step its input went bad.  (The reference yields NaN exactly in the outputs
+ * that depend on the bad input -- every torque of rnea; H and J keep the entries that do
+ * not; these kernels poison the whole configuration.)  The single-configuration ABI
+ * (rigidbody.h) computes every finite angle exactly, as the reference, and returns NaN
+ * outputs for NaN / Inf inputs.
  */
 #ifndef RIGIDBODY_BATCH_H
 #define RIGIDBODY_BATCH_H
@@ -119,21 +136,28 @@ int multibody_kernel_path(const Multibody *mb, int kind, int f64);
 int multibody_rnea_kernel_path(const Multibody *mb, int f64);
 /* The launch form of that kernel (same resolution, compiles it if needed): 0 = precompiled
  * generic kernel, else the model-specialised kernel's configurations-per-lane form -- 1 one per
- * lane, 2 two per lane on packed fp32, 3 two per lane one after the other (fp64 RNEA), 4 / 5
- * the bias / mass-matrix wave split packed / one per lane (fp32 mass-matrix forward dynamics
- * and rollouts at small batches).  Negative = -status on a bad argument. */
+ * lane, 2 two per lane on packed fp32, 3 two per lane one after the other (the fp64 RNEA from
+ * 2^19 configurations, and the fp32 RNEA of chains up to 8 links on the tiled layout from 2^19,
+ * compiled there with ordinary instead of non-temporal loads / stores), 4 / 5 the bias /
+ * mass-matrix wave split packed / one per lane (fp32 mass-matrix forward dynamics and rollouts
+ * up to 2^17 configurations).  Negative = -status on a bad argument. */
 int multibody_kernel_form_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled);
 /* Where the reference's single-configuration queries (rigidbody.h: rnea, crba, fwd_kin,
  * jac) run for this model: 0 = on the calling host thread (the GPU lane bodies compiled for
  * the host; serial revolute chains of a precompiled DOF on an FMA3/AVX2 CPU), 1 = one GPU
  * launch per call (trees / prismatic joints, or rb_set_tuning("single_gpu", 1)). */
 int multibody_single_config_path(const Multibody *mb);
-/* The generated source of a model-specialised kernel in its large-batch SoA form (the
- * lane form of a 2^20-configuration SoA launch; returns its length; copies at most cap-1
- * bytes + NUL into buf when buf != NULL). */
+/* The generated source of the model-specialised kernel a launch of `batch` configurations
+ * (tiled != 0: the *_tiled entry points) runs -- the same form, tail and load / store policy
+ * multibody_kernel_form_ex reports; returns its length; copies at most cap-1 bytes + NUL into
+ * buf when buf != NULL.  multibody_jit_source = a 2^20-configuration SoA launch. */
+int multibody_jit_source_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled, char *buf,
+                            int64_t cap);
 int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap);
 /* hipRTC-compiles that kernel for `arch` (NULL = "gfx950") without a device; returns
  * the code-object size, or minus an rb_status code (log in rb_last_error()). */
+int64_t multibody_jit_compile_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled,
+                                 const char *arch);
 int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char *arch);
 
 void multibody_result_free(double *p);

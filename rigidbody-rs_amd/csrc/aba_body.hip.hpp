@@ -14,7 +14,12 @@ namespace dev {
 
 template <typename T, int N, bool FAST, typename Out>
 RB_HD void aba_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
-                                         Out &&out) {
+                                         Out &&out_) {
+    InputGuard<T> gd;  // out-of-domain configurations: NaN accelerations (spatial.hip.hpp)
+    gd.template joints<SerialTopo>(qv);
+    gd.vals(qdv);
+    gd.vals(tv);
+    auto out = [&](int j, T v) { out_(j, gd.out(v)); };
     T cs[N], sn[N];
     T cw0[N], cw1[N], cv0[N], cv1[N];  // c_i = v_i x (S qd_i): (w.y qd, -w.x qd, 0; v.y qd, -v.x qd, 0)
     V3<T> pn[N], pf[N];                // bias force p_i = v_i x* (I_i v_i)
@@ -414,9 +419,10 @@ __device__ __forceinline__ void rollout_split_block2(const f2 *mdl, float *__res
                 qv[j] = sx[j][l];
                 qdv[j] = sx[N + j][l];
             }
-            fdh_bias<f2, N, FAST>(mdl, qv, qdv, cs, sn, C);
+            InputGuard<f2> gd;  // the state's domain, every step (fdh_split_block2)
+            fdh_bias<f2, N, FAST>(mdl, qv, qdv, cs, sn, C, gd);
 #pragma unroll
-            for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
+            for (int j = 0; j < N; ++j) shC[g][j][l] = gd.out(C[j]);
             __syncthreads();  // A
             __syncthreads();  // B
         } else {
@@ -438,8 +444,10 @@ __device__ __forceinline__ void rollout_split_block2(const f2 *mdl, float *__res
             __syncthreads();  // A
 #pragma unroll
             for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
+            InputGuard<f2> gd;
+            gd.vals(tv);
             fdh_solve<f2, N>(H, Di, tv, C, [&](int j, f2 a) {
-                const f2 qdn = fmadd(dt2, a, sx[N + j][l]);
+                const f2 qdn = fmadd(dt2, gd.out(a), sx[N + j][l]);
                 const f2 qn = fmadd(dt2, qdn, sx[j][l]);
                 sx[N + j][l] = qdn;
                 sx[j][l] = qn;

@@ -215,8 +215,11 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
         const rbamd::JitKernel *res = it->second.function ? &it->second : nullptr;
         if (rbamd::tuning_generation() != gen) continue;
         if (slot && res) {
-            Multibody::JitPub &rec = mb->jit_pub[{(const void *)slot, res}];
-            rec.jk = res;
+            // jk is written once, when the record is created (the key holds the same pointer), and
+            // never again: fast-path readers may hold the record while this re-stamps gen
+            auto ins = mb->jit_pub.try_emplace({(const void *)slot, res});
+            Multibody::JitPub &rec = ins.first->second;
+            if (ins.second) rec.jk = res;
             rec.gen.store(gen, std::memory_order_release);
             slot->store(&rec, std::memory_order_release);
         }
@@ -229,15 +232,35 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
 // 1024 SIMDs x 64 lanes x 2) the one-per-lane kernel keeps more of the chip busy.
 constexpr uint32_t kSeqMinBatch = 1u << 19;
 
-const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, bool fast, uint32_t B, bool tiled) {
+// The hipRTC kernel variant a launch takes: configurations per lane (0 = the jit_pack policy),
+// the sequential pair's one-per-lane tail, the non-temporal override and the fp32 trig form.
+// The launch paths and the inspection entry points (multibody_jit_source_ex) share it.
+struct JitShape {
+    int pack = 0, tail = 0, nt = -1;
+    bool fast = false;
+};
+JitShape jit_shape(const Multibody *mb, rbamd::JitKind kind, bool f64, uint32_t B, bool tiled);
+
+const rbamd::JitKernel *jit_shaped(const Multibody *mb, rbamd::JitKind kind, bool f64, uint32_t B, bool tiled) {
+    const JitShape sh = jit_shape(mb, kind, f64, B, tiled);
+    return jit_get(mb, kind, f64, sh.fast, sh.pack, sh.tail, sh.nt);
+}
+
+JitShape rnea_shape(const Multibody *mb, bool f64, uint32_t B, bool tiled) {
     // fp32 chains up to 8 links on the tiled layout at large batches: the sequential pair too
     // (FR3 2^20 22.0-22.1 vs 22.3-24.0 us on two boxes, profiles/r04/ab/ab_r32_seq*.log), with
     // ordinary (temporal) loads and stores (tuning.hpp rnea_nt; the 30-link chain and the 14-DOF
     // tree keep nt = 3)
     const bool big32 = !f64 && tiled && B >= kSeqMinBatch && mb->model.n <= 8;
-    const int pack = rbamd::tuning().pack >= 0 ? 0 : big32 ? 3 : B < kSeqMinBatch ? 1 : 0;
-    const int nt = (big32 && rbamd::tuning().rnea_nt < 0) ? 0 : -1;
-    return jit_get(mb, rbamd::JitKind::Rnea, f64, fast, pack, rbamd::jit_seq_tail(tiled), nt);
+    JitShape sh;
+    sh.pack = rbamd::tuning().pack >= 0 ? 0 : big32 ? 3 : B < kSeqMinBatch ? 1 : 0;
+    sh.nt = (big32 && rbamd::tuning().rnea_nt < 0) ? 0 : -1;
+    sh.tail = rbamd::jit_seq_tail(tiled);
+    return sh;
+}
+
+const rbamd::JitKernel *jit_rnea(const Multibody *mb, bool f64, uint32_t B, bool tiled) {
+    return jit_shaped(mb, rbamd::JitKind::Rnea, f64, B, tiled);
 }
 
 // A tree / prismatic model has no precompiled kernel: without its hipRTC kernel the launch
@@ -270,7 +293,7 @@ constexpr uint32_t kSplitMaxBatch = 1u << 17;
 
 // The forward-dynamics kernel a launch of B configurations takes (auto policy when the
 // tuning `pack` is unset).
-const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, bool fast, uint32_t B) {
+int fd_pack(const Multibody *mb, bool f64, uint32_t B) {
     int pack = 0;
     if (rbamd::tuning().pack < 0) {
         if (!f64 && rbamd::jit_fd_form(mb->model) == 2)
@@ -278,7 +301,11 @@ const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, bool fast, uint32_
         else  // paired lanes halve the grid: below kPackMinBatch one per lane fills more CUs
             pack = B < kPackMinBatch ? 1 : 0;
     }
-    return jit_get(mb, rbamd::JitKind::Fd, f64, fast, pack);
+    return pack;
+}
+
+const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, uint32_t B) {
+    return jit_shaped(mb, rbamd::JitKind::Fd, f64, B, false);
 }
 
 // The rollout kernel a launch of B configurations takes: fp32 mass-matrix rollouts up to 2^17
@@ -286,10 +313,27 @@ const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, bool fast, uint32_
 // rollout_split_block2), as jit_fd's small-batch forward dynamics.  FR3, K = 16, HIP graph:
 // 16384 43.3 vs 62.7 us (pair), 65536 43.6 vs 63.5, 131072 58.9 vs 63.7; 262144 101.5 vs 93.2
 // (profiles/r03/rollout_split/).
-const rbamd::JitKernel *jit_rollout(const Multibody *mb, bool f64, bool fast, uint32_t B) {
-    const int pack = (rbamd::tuning().pack < 0 && !f64 && B <= kSplitMaxBatch &&
-                      rbamd::jit_fd_form(mb->model) == 2 && !(rbamd::tuning().jit_variant & 256)) ? 4 : 0;
-    return jit_get(mb, rbamd::JitKind::Rollout, f64, fast, pack);
+int rollout_pack(const Multibody *mb, bool f64, uint32_t B) {
+    return (rbamd::tuning().pack < 0 && !f64 && B <= kSplitMaxBatch && rbamd::jit_fd_form(mb->model) == 2 &&
+            !(rbamd::tuning().jit_variant & 256)) ? 4 : 0;
+}
+
+const rbamd::JitKernel *jit_rollout(const Multibody *mb, bool f64, uint32_t B) {
+    return jit_shaped(mb, rbamd::JitKind::Rollout, f64, B, false);
+}
+
+JitShape jit_shape(const Multibody *mb, rbamd::JitKind kind, bool f64, uint32_t B, bool tiled) {
+    JitShape sh;
+    switch (kind) {
+        case rbamd::JitKind::Rnea: sh = rnea_shape(mb, f64, B, tiled); break;
+        case rbamd::JitKind::Fd: sh.pack = fd_pack(mb, f64, B); break;
+        case rbamd::JitKind::Rollout: sh.pack = rollout_pack(mb, f64, B); break;
+        default: break;
+    }
+    // CRBA evaluates its angles with the precise fp32 sincos; every other kind with the fast one
+    // unless RB_FAST_TRIG=0 (fp64 always its own)
+    sh.fast = kind != rbamd::JitKind::Crba && fast_trig() && !f64;
+    return sh;
 }
 
 unsigned jit_grid(const rbamd::JitKernel *jk, uint32_t B) {
@@ -316,7 +360,7 @@ template <typename T>
 hipError_t launch_rnea_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *qdd, T *tau,
                            uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, fast_trig(), B, tiled)) {
+    if (const rbamd::JitKernel *jk = jit_rnea(mb, sizeof(T) == 8, B, tiled)) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q, (void *)&qd, (void *)&qdd, (void *)&tau, (void *)&B, (void *)&lda, (void *)&bs};
         return jit_launch(jk, B, args, s);
@@ -329,7 +373,7 @@ template <typename T>
 hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *tau, T *qdd,
                          uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_fd(mb, sizeof(T) == 8, fast_trig(), B)) {
+    if (const rbamd::JitKernel *jk = jit_fd(mb, sizeof(T) == 8, B)) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau, (void *)&qdd, (void *)&B, (void *)&lda, (void *)&bs};
         return jit_launch(jk, B, args, s);
@@ -342,7 +386,7 @@ template <typename T>
 hipError_t launch_rollout_any(const Multibody *mb, const T *mdl, T *q, T *qd, const T *tau_seq, T dt, int K, T *traj,
                               uint32_t B, int64_t ld, hipStream_t s) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_rollout(mb, sizeof(T) == 8, fast_trig(), B)) {
+    if (const rbamd::JitKernel *jk = jit_rollout(mb, sizeof(T) == 8, B)) {
         void *args[] = {(void *)&q, (void *)&qd, (void *)&tau_seq, (void *)&dt, (void *)&K, (void *)&traj,
                         (void *)&B, (void *)&ld};
         return jit_launch(jk, B, args, s);
@@ -853,9 +897,9 @@ const rbamd::JitKernel *resolve_kernel(const Multibody *mb, int kind, bool f64, 
     if (kind >= 4 && kin_precompiled(mb)) return nullptr;  // precompiled kinematics
     if (!rbamd::jit_enabled()) return nullptr;
     const uint32_t B = batch < kChunk ? (uint32_t)batch : (uint32_t)kChunk;
-    if (kind == 0) return jit_rnea(mb, f64, fast_trig(), B, tiled);
-    if (kind == 1) return jit_fd(mb, f64, fast_trig(), B);
-    if (kind == 3) return jit_rollout(mb, f64, fast_trig(), B);
+    if (kind == 0) return jit_rnea(mb, f64, B, tiled);
+    if (kind == 1) return jit_fd(mb, f64, B);
+    if (kind == 3) return jit_rollout(mb, f64, B);
     if (kind >= 4) return jit_kin(mb, kind == 5, f64);
     return jit_get(mb, rbamd::JitKind::Crba, f64, false);
 }
@@ -865,6 +909,22 @@ int check_kernel_query(const Multibody *mb, int kind, int64_t batch) {
     if (kind < 0 || kind > 5) return set_err(RB_ERR_ARG, kKindMsg);
     if (batch < 1) return set_err(RB_ERR_ARG, "batch must be positive");
     return RB_OK;
+}
+
+// The (pack, tail) jit_get resolves a shape to (the kernel's actual form).
+void resolve_pack(const Multibody *mb, rbamd::JitKind kind, bool f64, const JitShape &sh, int *pk, int *tl) {
+    *pk = sh.pack > 0 ? sh.pack : rbamd::jit_model_pack(mb->model, kind, f64, 0);
+    *tl = (kind == rbamd::JitKind::Rnea && *pk == 3) ? sh.tail : 0;
+}
+
+// The hipRTC source of the kernel a launch of `batch` configurations (tiled or SoA) would run.
+std::string shaped_source(const Multibody *mb, int kind, bool f64, int64_t batch, bool tiled) {
+    const uint32_t B = batch < kChunk ? (uint32_t)batch : (uint32_t)kChunk;
+    const auto k = (rbamd::JitKind)kind;
+    const JitShape sh = jit_shape(mb, k, f64, B, tiled);
+    int pk = 0, tl = 0;
+    resolve_pack(mb, k, f64, sh, &pk, &tl);
+    return rbamd::jit_source(mb->model, k, f64, sh.fast, pk, tl, sh.nt);
 }
 
 void note_jit_errors(const Multibody *mb) {
@@ -899,10 +959,12 @@ int multibody_single_config_path(const Multibody *mb) {
 }
 
 int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap) {
-    if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
-    const std::string src = rbamd::jit_source(mb->model, (rbamd::JitKind)kind, f64 != 0,
-                                              kind != 2 && fast_trig() && !f64);
+    return multibody_jit_source_ex(mb, kind, f64, int64_t(1) << 20, 0, buf, cap);
+}
+
+int multibody_jit_source_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled, char *buf, int64_t cap) {
+    if (int rc = check_kernel_query(mb, kind, batch)) return -rc;
+    const std::string src = shaped_source(mb, kind, f64 != 0, batch, tiled != 0);
     if (buf && cap > 0) {
         const size_t n = src.size() < (size_t)(cap - 1) ? src.size() : (size_t)(cap - 1);
         std::memcpy(buf, src.data(), n);
@@ -912,12 +974,19 @@ int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int6
 }
 
 int64_t multibody_jit_compile(const Multibody *mb, int kind, int f64, const char *arch) {
-    if (!mb) return -set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 5) return -set_err(RB_ERR_ARG, kKindMsg);
+    return multibody_jit_compile_ex(mb, kind, f64, int64_t(1) << 20, 0, arch);
+}
+
+int64_t multibody_jit_compile_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled, const char *arch) {
+    if (int rc = check_kernel_query(mb, kind, batch)) return -rc;
+    const uint32_t B = batch < kChunk ? (uint32_t)batch : (uint32_t)kChunk;
+    const auto k = (rbamd::JitKind)kind;
+    const JitShape sh = jit_shape(mb, k, f64 != 0, B, tiled != 0);
+    int pk = 0, tl = 0;
+    resolve_pack(mb, k, f64 != 0, sh, &pk, &tl);
     std::vector<char> code;
     std::string err;
-    if (!rbamd::jit_compile(mb->model, (rbamd::JitKind)kind, f64 != 0, kind != 2 && fast_trig() && !f64,
-                            arch ? arch : "gfx950", &code, &err))
+    if (!rbamd::jit_compile(mb->model, k, f64 != 0, sh.fast, arch ? arch : "gfx950", &code, &err, pk, tl, sh.nt))
         return -set_err(RB_ERR_HIP, err);
     return (int64_t)code.size();
 }

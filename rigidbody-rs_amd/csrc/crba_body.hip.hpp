@@ -49,10 +49,13 @@ RB_HD void crba_core(const T *mdl, const T (&cs)[N], const T (&sn)[N], Out &&out
 
 template <typename T, int N, bool FAST, typename Out>
 RB_HD void crba_eval(const T *mdl, const T (&qv)[N], Out &&out) {
+    InputGuard<T> gd;  // out-of-domain configurations: NaN upper triangle (spatial.hip.hpp)
+    gd.template joints<SerialTopo>(qv);
     T cs[N], sn[N];
 #pragma unroll
     for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);
-    crba_core<T, N>(mdl, cs, sn, static_cast<Out &&>(out));
+    // strictly-lower entries (row > col) stay the ABI's exact zeros
+    crba_core<T, N>(mdl, cs, sn, [&](int e, T v) { out(e, e % N <= e / N ? gd.out(v) : v); });
 }
 
 template <typename T, int N, bool FAST, typename Topo = SerialTopo>

@@ -38,14 +38,16 @@ namespace dev {
 // (cos, sin) the later stages reuse.  Model-specialised kernels with signed-permutation R_p and
 // centre-of-mass link forces take the fused backward sweep (rnea_body.hip.hpp rnea_bwd_g: the
 // link force's mass scaling and the child accumulations as FMAs; FR3 fp64 5 fewer VALU per link).
+// gd: the input check of q and qd (rnea_fwd, InputGuard).
 template <typename T, int N, bool FAST>
-RB_HD void fdh_bias(const T *mdl, const T (&qv)[N], const T (&qdv)[N], T (&cs)[N], T (&sn)[N], T (&C)[N]) {
+RB_HD void fdh_bias(const T *mdl, const T (&qv)[N], const T (&qdv)[N], T (&cs)[N], T (&sn)[N], T (&C)[N],
+                    InputGuard<T> &gd) {
     V3<T> fn[N], ff[N];  // ff: the link force, or g = f / m (kRneaGForm)
     RneaState<T> st;
-    rnea_fwd0<T, FAST, kRneaGForm>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0]);
+    rnea_fwd0<T, FAST, kRneaGForm>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0], gd);
 #pragma unroll
     for (int j = 1; j < N; ++j)
-        rnea_fwd<T, FAST, kRneaGForm>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j]);
+        rnea_fwd<T, FAST, kRneaGForm>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j], gd);
     reload_fence();
     RB_STAGE("bias_bwd");
     if constexpr (kRneaGForm) {
@@ -127,14 +129,16 @@ RB_HD void fdh_solve(const T (&H)[N][N], const T (&Di)[N], const T (&tv)[N], con
 template <typename T, int N, bool FAST, typename Tau, typename Out>
 RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&load_tau, Out &&out) {
     T cs[N], sn[N], C[N], tv[N], H[N][N], Di[N];
+    InputGuard<T> gd;  // out-of-domain configurations: NaN accelerations (spatial.hip.hpp)
     if constexpr (RB_FDH_TAU_AT == 0) load_tau(tv);
     RB_STAGE("bias_fwd");
-    fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C);
+    fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C, gd);
     if constexpr (RB_FDH_TAU_AT == 1) load_tau(tv);
     fdh_factor<T, N>(mdl, cs, sn, H, Di);
     if constexpr (RB_FDH_TAU_AT >= 2) load_tau(tv);
+    gd.vals(tv);
     RB_STAGE("solve");
-    fdh_solve<T, N>(H, Di, tv, C, static_cast<Out &&>(out));
+    fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) { out(j, gd.out(v)); });
 }
 
 // Lane body: loads in first-use order (q, qd root->leaf, then tau), as aba_lane.
@@ -242,9 +246,10 @@ __device__ __forceinline__ void fdh_split_block2(const f2 *mdl, const float *__r
             qdv[j] = ld_row2(qd + o, j * ld, offA, offB);
             __builtin_amdgcn_sched_barrier(0);
         }
-        fdh_bias<f2, N, FAST>(mdl, qv, qdv, cs, sn, C);
+        InputGuard<f2> gd;  // out-of-domain configurations: C, and so every qdd, NaN
+        fdh_bias<f2, N, FAST>(mdl, qv, qdv, cs, sn, C, gd);
 #pragma unroll
-        for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
+        for (int j = 0; j < N; ++j) shC[g][j][l] = gd.out(C[j]);
         __syncthreads();
     } else {
         f2 qv[N], tv[N], cs[N], sn[N], C[N], H[N][N], Di[N];
@@ -272,8 +277,12 @@ __device__ __forceinline__ void fdh_split_block2(const f2 *mdl, const float *__r
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
+        // a NaN in C (the bias wave's guard) reaches every qdd through the solve: every
+        // y_i = tau_i - C_i is NaN, so is every forward and back substitution value
+        InputGuard<f2> gd;
+        gd.vals(tv);
         fdh_solve<f2, N>(H, Di, tv, C, [&](int j, f2 v) {
-            if (liveA) st_row2(qdd + o, j * ld, offA, offB, v);
+            if (liveA) st_row2(qdd + o, j * ld, offA, offB, gd.out(v));
         });
     }
 }
@@ -305,9 +314,10 @@ __device__ __forceinline__ void fdh_split_block1(const T *mdl, const T *__restri
             qdv[j] = ld_row(qd + o, j * ld, off);
             __builtin_amdgcn_sched_barrier(0);
         }
-        fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C);
+        InputGuard<T> gd;  // as fdh_split_block2
+        fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C, gd);
 #pragma unroll
-        for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
+        for (int j = 0; j < N; ++j) shC[g][j][l] = gd.out(C[j]);
         __syncthreads();
     } else {
         T qv[N], tv[N], cs[N], sn[N], C[N], H[N][N], Di[N];
@@ -332,8 +342,10 @@ __device__ __forceinline__ void fdh_split_block1(const T *mdl, const T *__restri
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
+        InputGuard<T> gd;
+        gd.vals(tv);
         fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) {
-            if (live) st_row(qdd + o, j * ld, off, v);
+            if (live) st_row(qdd + o, j * ld, off, gd.out(v));
         });
     }
 }

@@ -3,6 +3,7 @@
 
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -67,6 +68,9 @@ int jit_waves(JitKind kind, bool f64, int n) {
     const int v = tuning().jit_waves;
     if (v >= 0) return v;
     if (kind == JitKind::Rollout && !f64 && n <= 8) return jit_pack(kind, f64, n) != 1 ? 2 : 4;
+    // fp64 short-chain rollout: 126 VGPRs at the target, 129 (3 waves/SIMD) without it since the
+    // input checks (InputGuard, spatial.hip.hpp)
+    if (kind == JitKind::Rollout && f64 && n <= 8) return 4;
     return 0;
 }
 
@@ -148,6 +152,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
     o << "#define RB_OPAQUE_CONSTS " << (jit_opaque(kind, f64, m.n) ? 1 : 0) << "\n";
     if (kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack)) o << "#define RB_ROLLOUT_NO_HOIST 1\n";
+    // input checks pinned into the sweep's state (rnea_body.hip.hpp rnea_fwd)
+    if (kind == JitKind::Rollout || m.n > 8) o << "#define RB_GUARD_ANCHOR 1\n";
     // the rollout's forward dynamics follows the fd_form policy (mass-matrix form for short
     // serial chains) unless RB_VARIANT bit 8 (A/B) keeps the ABA
     if (kind == JitKind::Rollout && jit_fd_form(m) == 2 && !(tuning().jit_variant & 256))
@@ -195,7 +201,11 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     const bool com = dyn && !(kind == JitKind::Rnea && f64) && !(tuning().jit_variant & 512);
     // rnea_lane_park: fp32 one-per-lane RNEA of long serial chains in the centre-of-mass g-form
     // (signed-permutation frames), when the tuning asks for it
-    const int pk_req = tuning().rnea_park < 0 ? (m.n >= 20 ? 8 : 0) : tuning().rnea_park.load();
+    // the parked forces take NP x 6 KB of LDS per 4-wave block: at most kMaxPark links, so that 3
+    // blocks still fit a CU's 160 KB (gfx950) -- a requested count past it is clamped, not handed to
+    // hipRTC to fail on (which would leave the launch on the generic kernel)
+    constexpr int kMaxPark = (160 * 1024 / 3) / (4 * 6 * 64 * 4);
+    const int pk_req = std::min(kMaxPark, tuning().rnea_park < 0 ? (m.n >= 20 ? 8 : 0) : tuning().rnea_park.load());
     const int park = (kind == JitKind::Rnea && !f64 && pack == 1 && m.serial_revolute() && com &&
                       (sr > 0 || (sr < 0 && perm)) && pk_req > 0 && pk_req < m.n) ? pk_req : 0;
     if (com) {

@@ -24,6 +24,11 @@ __global__ __launch_bounds__(kBlock) void fwd_kin_kernel(const T *__restrict__ g
     q += (int64_t)blockIdx.x * bs_in;  // block k's rows (crba.hip)
     pos += (int64_t)blockIdx.x * bs_out;
     const uint32_t off = threadIdx.x * (uint32_t)sizeof(T);
+    T qv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) qv[j] = ld_row(q, j * ld, off);
+    InputGuard<T> gd;  // out-of-domain configurations: NaN outputs (spatial.hip.hpp)
+    gd.template joints<SerialTopo>(qv);
     // T_0 T_1 ... T_{n-1} accumulated from the base: p += R p_i, R = R E_i
     M3<T> R{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
     V3<T> p = v3(T(0), T(0), T(0));
@@ -31,7 +36,7 @@ __global__ __launch_bounds__(kBlock) void fwd_kin_kernel(const T *__restrict__ g
     for (int j = 0; j < N; ++j) {
         const Link<T> L = load_link(mdl, j);
         T s, c;
-        sin_cos<FAST>(ld_row(q, j * ld, off), s, c);
+        sin_cos<FAST>(qv[j], s, c);
         const M3<T> E = joint_rotation(L.Rp, c, s);
         p = mul_add(p, R, L.p);
         M3<T> Rn;
@@ -42,9 +47,9 @@ __global__ __launch_bounds__(kBlock) void fwd_kin_kernel(const T *__restrict__ g
                 Rn.m[3 * r + cc] = fmadd(R.m[3 * r + 0], E.m[cc], fmadd(R.m[3 * r + 1], E.m[3 + cc], R.m[3 * r + 2] * E.m[6 + cc]));
         R = Rn;
     }
-    st_row(pos, 0 * ld, off, p.x);
-    st_row(pos, 1 * ld, off, p.y);
-    st_row(pos, 2 * ld, off, p.z);
+    st_row(pos, 0 * ld, off, gd.out(p.x));
+    st_row(pos, 1 * ld, off, gd.out(p.y));
+    st_row(pos, 2 * ld, off, gd.out(p.z));
 }
 
 template <typename T, int N, bool FAST>
@@ -59,6 +64,12 @@ __global__ __launch_bounds__(kBlock) void jac_kernel(const T *__restrict__ gmdl,
     q += (int64_t)blockIdx.x * bs_in;
     J += (int64_t)blockIdx.x * bs_out;
     const uint32_t off = threadIdx.x * (uint32_t)sizeof(T);
+    // every angle first: a bad one poisons all columns, also those stored before it is used
+    T qv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) qv[j] = ld_row(q, j * ld, off);
+    InputGuard<T> gd;  // out-of-domain configurations: NaN outputs (spatial.hip.hpp)
+    gd.template joints<SerialTopo>(qv);
     // acc = pose of the last frame in frame i, built leaf -> root (multibody.rs:97-106):
     // column i = motion transform of S_i = (0,0,1 | 0) by acc:
     //   rot = R^T z,  lin = R^T (0 - p x z) = -R^T (p.y, -p.x, 0)
@@ -72,15 +83,15 @@ __global__ __launch_bounds__(kBlock) void jac_kernel(const T *__restrict__ gmdl,
     for (int i = N - 1; i >= 0; --i) {
         const V3<T> rot = v3(R.m[6], R.m[7], R.m[8]);
         const V3<T> lin = mul_t(R, v3(-p.y, p.x, T(0)));
-        st_row(J, (6 * i + 0) * ld, off, lin.x);
-        st_row(J, (6 * i + 1) * ld, off, lin.y);
-        st_row(J, (6 * i + 2) * ld, off, lin.z);
-        st_row(J, (6 * i + 3) * ld, off, rot.x);
-        st_row(J, (6 * i + 4) * ld, off, rot.y);
-        st_row(J, (6 * i + 5) * ld, off, rot.z);
+        st_row(J, (6 * i + 0) * ld, off, gd.out(lin.x));
+        st_row(J, (6 * i + 1) * ld, off, gd.out(lin.y));
+        st_row(J, (6 * i + 2) * ld, off, gd.out(lin.z));
+        st_row(J, (6 * i + 3) * ld, off, gd.out(rot.x));
+        st_row(J, (6 * i + 4) * ld, off, gd.out(rot.y));
+        st_row(J, (6 * i + 5) * ld, off, gd.out(rot.z));
         const Link<T> L = load_link(mdl, i);
         T s, c;
-        sin_cos<FAST>(ld_row(q, i * ld, off), s, c);
+        sin_cos<FAST>(qv[i], s, c);
         const M3<T> E = joint_rotation(L.Rp, c, s);
         // acc <- T_i * acc = (E R, p_i + E p)
         p = mul_add(L.p, E, p);

@@ -17,14 +17,27 @@ struct RneaState {
 
 // Link 0: v_{-1} = 0, a_{-1} = (0, (0,0,+g)) -- multibody.rs:116-120
 // GF (centre-of-mass form only): ff receives g = f / m (spatial.hip.hpp link_force_g).
+// Each step checks its link's inputs into gd (InputGuard, spatial.hip.hpp) where it consumes them.
+// RB_GUARD_ANCHOR (jit.cpp: rollouts and chains longer than 8 links) also adds the running check
+// -- +-0 while every input so far was in range -- to w.z: that use pins each link's check next to
+// its work, where the scheduler would otherwise sink the checks towards the stores and keep the
+// input rows live across the sweep (30-link fp32 parked RNEA: 151 VGPRs anchored, 168 + 200 B of
+// scratch not; fp64 FR3 rollout 127 vs 129, the 4th wave per SIMD).  Short-chain RNEA / FD
+// kernels are tighter without it (fp64 FR3 RNEA pair 127 vs 135 VGPRs).
+#ifndef RB_GUARD_ANCHOR
+#define RB_GUARD_ANCHOR 0
+#endif
 template <typename T, bool FAST, bool GF = false>
 RB_HD void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn, T &cs,
-                                          V3<T> &fn, V3<T> &ff) {
+                                          V3<T> &fn, V3<T> &ff, InputGuard<T> &gd) {
     const Link<T> L = load_link(mdl, 0);
+    gd.angle(q0);
+    gd.val(qd0);
+    gd.val(qdd0);
     sin_cos<FAST>(q0, sn, cs);
     const M3<T> E = joint_rotation(L.Rp, cs, sn);
     const T g = T(kGravity);
-    st.w = v3(T(0), T(0), qd0);
+    st.w = v3(T(0), T(0), RB_GUARD_ANCHOR ? gd.out(qd0) : qd0);
     st.v = v3(T(0), T(0), T(0));
     st.aw = v3(T(0), T(0), qdd0);
     st.av = v3(g * E.m[6], g * E.m[7], g * E.m[8]);  // E^T (0,0,g)
@@ -40,8 +53,11 @@ RB_HD void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn,
 // Link j >= 1: forward sweep step (multibody.rs:122-141).
 template <typename T, bool FAST, bool GF = false>
 RB_HD void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, T &sn, T &cs,
-                                         V3<T> &fn, V3<T> &ff) {
+                                         V3<T> &fn, V3<T> &ff, InputGuard<T> &gd) {
     const Link<T> L = load_link(mdl, j);
+    gd.angle(qj);
+    gd.val(qdj);
+    gd.val(qddj);
     sin_cos<FAST>(qj, sn, cs);
     const M3<T> E = joint_rotation(L.Rp, cs, sn);
     // SpatialVelocity::transform (spatial.rs:110-116) on v and a
@@ -50,6 +66,7 @@ RB_HD void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, 
     V3<T> wn = mul_t(E, st.w), vn = mul_t(E, u);
     V3<T> awn = mul_t(E, st.aw), avn = mul_t(E, ua);
     wn.z += qdj;        // multibody.rs:130
+    if constexpr (RB_GUARD_ANCHOR != 0) wn.z = gd.out(wn.z);
     awn.z += qddj;      // multibody.rs:133
     avn.x = fmadd(vn.y, qdj, avn.x);   // multibody.rs:135-138, v x (z qd) unrolled
     avn.y = fmadd(-vn.x, qdj, avn.y);
@@ -114,24 +131,38 @@ RB_HD void rnea_bwd_g(const T *mdl, const T (&cs)[N], const T (&sn)[N], const V3
     out(0, n.z);
 }
 
+template <typename T>
+RB_HD void poison_leaf(const InputGuard<T> &gd, V3<T> &n, V3<T> &f) {
+    n = v3(gd.out(n.x), gd.out(n.y), gd.out(n.z));
+    f = v3(gd.out(f.x), gd.out(f.y), gd.out(f.z));
+}
+
 // Forward sweep (multibody.rs:122-141) then backward sweep (143-150), fused: the
 // per-link forces never leave registers.  One call evaluates the configuration whose
 // joint values are in (qv, qdv, qddv) and hands tau_j to `out(j, value)`.
 template <typename T, int N, bool FAST, typename Out>
 RB_HD void rnea_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
-                                          const T (&qddv)[N], Out &&out) {
+                                          const T (&qddv)[N], Out &&out_) {
+    InputGuard<T> gd;  // out-of-domain configurations: NaN torques (spatial.hip.hpp)
+    // short chains poison the n outputs, long ones the leaf's wrench (below)
+    constexpr bool kLeaf = N > 8;
+    auto out = [&](int j, T v) { out_(j, kLeaf ? v : gd.out(v)); };
     T cs[N], sn[N];
     V3<T> fn[N], ff[N];  // per-link spatial force: moment n (rot), force f (lin) -- or g = f / m
     RneaState<T> st;
-    rnea_fwd0<T, FAST, kRneaGForm>(mdl, qv[0], qdv[0], qddv[0], st, sn[0], cs[0], fn[0], ff[0]);
+    rnea_fwd0<T, FAST, kRneaGForm>(mdl, qv[0], qdv[0], qddv[0], st, sn[0], cs[0], fn[0], ff[0], gd);
 #pragma unroll
     for (int j = 1; j < N; ++j)
-        rnea_fwd<T, FAST, kRneaGForm>(mdl, j, qv[j], qdv[j], qddv[j], st, sn[j], cs[j], fn[j], ff[j]);
+        rnea_fwd<T, FAST, kRneaGForm>(mdl, j, qv[j], qdv[j], qddv[j], st, sn[j], cs[j], fn[j], ff[j], gd);
 
+    // Long chains: the input check poisons the leaf's wrench; the backward sweep carries a
+    // fully-NaN wrench to every parent (each row of E = R_p Rz(q) has an entry that is not a
+    // folded zero), so every tau is NaN -- 6 adds where poisoning the outputs takes n.
+    if constexpr (kLeaf) poison_leaf(gd, fn[N - 1], ff[N - 1]);
     // Backward sweep: tau_i = n_i.z (multibody.rs:144)
     reload_fence();
     if constexpr (kRneaGForm) {
-        rnea_bwd_g<T, N>(mdl, cs, sn, fn, ff, static_cast<Out &&>(out));
+        rnea_bwd_g<T, N>(mdl, cs, sn, fn, ff, out);
         return;
     }
 #pragma unroll
@@ -211,6 +242,7 @@ __device__ __forceinline__ void rnea_lane_park(const T *mdl, const T *__restrict
         qdv[j] = ld_row(qd, j * ld, off);
         qddv[j] = ld_row(qdd, j * ld, off);
     }
+    InputGuard<T> gd;  // out-of-domain configurations: NaN torques (spatial.hip.hpp)
     V3<T> fn[N], gg[N];  // entries j < NP live in LDS after the forward sweep
     auto put = [&](int j) {
         const T v[6] = {fn[j].x, fn[j].y, fn[j].z, gg[j].x, gg[j].y, gg[j].z};
@@ -219,13 +251,14 @@ __device__ __forceinline__ void rnea_lane_park(const T *mdl, const T *__restrict
     };
     RneaState<T> st;
     T sn, cs;
-    rnea_fwd0<T, FAST, true>(mdl, qv[0], qdv[0], qddv[0], st, sn, cs, fn[0], gg[0]);
+    rnea_fwd0<T, FAST, true>(mdl, qv[0], qdv[0], qddv[0], st, sn, cs, fn[0], gg[0], gd);
     put(0);
 #pragma unroll
     for (int j = 1; j < N; ++j) {
-        rnea_fwd<T, FAST, true>(mdl, j, qv[j], qdv[j], qddv[j], st, sn, cs, fn[j], gg[j]);
+        rnea_fwd<T, FAST, true>(mdl, j, qv[j], qdv[j], qddv[j], st, sn, cs, fn[j], gg[j], gd);
         if (j < NP) put(j);
     }
+    poison_leaf(gd, fn[N - 1], gg[N - 1]);  // as rnea_eval
     reload_fence();
     T qr[N];
 #pragma unroll

@@ -392,6 +392,15 @@ RB_HD void reload_fence() { asm volatile("" ::: "memory"); }
 // |x| < 2^20 rad -- far beyond any joint angle).  FAST=true (fp32 only) uses the
 // hardware v_sin_f32/v_cos_f32.
 RB_HD void sincos_cw(double x, double &s, double &c) {
+#if !defined(__HIP_DEVICE_COMPILE__) && !defined(__HIPCC_RTC__)
+    // host single-configuration path: past the reduction's exact range (and for NaN / Inf) the
+    // C library, as the reference's from_scaled_axis -- any finite angle is exact there
+    if (!(__builtin_fabs(x) < 0x1p45)) {
+        s = __builtin_sin(x);
+        c = __builtin_cos(x);
+        return;
+    }
+#endif
     const double k = __builtin_rint(x * 6.36619772367581382433e-01);  // 2/pi
     double r = __builtin_fma(-k, 1.57079632679489655800e+00, x);      // pi/2 hi
     r = __builtin_fma(-k, 6.12323399573676603587e-17, r);              // pi/2 mid
@@ -434,10 +443,46 @@ RB_HD void sincos_cw(float x, float &s, float &c) {
     c = ((q + 1) & 2) ? -cc : cc;
 }
 
+// FAST fp32: the hardware v_sin_f32 / v_cos_f32, which take revolutions.  The angle is reduced
+// to revolutions exactly first: k = rint(x / 2pi) from the 1.5 * 2^23 shifter, then
+// u = x (1/2pi)_hi - k + x (1/2pi)_lo with the first two terms in one FMA (x (1/2pi)_hi and k
+// agree in their leading bits, so the FMA's single rounding leaves u accurate to its own ulp).
+// A plain x * (1/2pi) carries a relative error of 2^-24 into the revolutions -- 6e-6 rad at
+// |x| = 100 -- and past 256 revolutions the instruction's input range is exceeded; the reduced
+// form keeps |q| <= pi accuracy for every |x| < 2^22 * 2 pi (the supported range is 2^22 rad,
+// InputGuard).  4 VALU per angle instead of 1 (packed pairs: 4 v_pk per pair).
+constexpr float kInv2PiHi = 0x1.45f306p-3f, kInv2PiLo = 0x1.b93910p-28f;  // 1/2pi = hi + lo + 7e-17
+constexpr float kRevShifter = 0x1.8p23f;                                 // 1.5 * 2^23
+RB_HD void sincos_hw(float x, float &s, float &c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float k = __builtin_fmaf(x, kInv2PiHi, kRevShifter) - kRevShifter;
+    const float u = __builtin_fmaf(x, kInv2PiLo, __builtin_fmaf(x, kInv2PiHi, -k));
+    s = __builtin_amdgcn_sinf(u);
+    c = __builtin_amdgcn_cosf(u);
+#else
+    sincos_cw(x, s, c);
+#endif
+}
+RB_HD void sincos_hw(f2 x, f2 &s, f2 &c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const f2 hi = f2{kInv2PiHi, kInv2PiHi}, lo = f2{kInv2PiLo, kInv2PiLo}, sh = f2{kRevShifter, kRevShifter};
+    const f2 k = fmadd(x, hi, sh) - sh;
+    const f2 u = fmadd(x, lo, fmadd(x, hi, -k));
+    s = f2{__builtin_amdgcn_sinf(u.x), __builtin_amdgcn_sinf(u.y)};
+    c = f2{__builtin_amdgcn_cosf(u.x), __builtin_amdgcn_cosf(u.y)};
+#else
+    float s0, c0, s1, c1;
+    sincos_cw(x.x, s0, c0);
+    sincos_cw(x.y, s1, c1);
+    s = f2{s0, s1};
+    c = f2{c0, c1};
+#endif
+}
+
 template <bool FAST>
 RB_HD void sin_cos(float x, float &s, float &c) {
     if constexpr (FAST) {
-        __sincosf(x, &s, &c);
+        sincos_hw(x, s, c);
     } else {
         sincos_cw(x, s, c);
     }
@@ -463,10 +508,10 @@ struct alignas(16) SinCosEntry {
 __shared__ SinCosEntry rb_sctab[256];
 
 // Every wave of the block must call this before any sin_cos(double) (it ends in a barrier);
-// blocks are 256 threads, one entry each.
+// any block size (one entry per thread for the 256-thread blocks every JIT kernel uses).
 __device__ __forceinline__ void sctab_init() {
-    const uint32_t t = threadIdx.x;
-    rb_sctab[t] = SinCosEntry{rb_sctab_src[2 * t], rb_sctab_src[2 * t + 1]};
+    for (uint32_t t = threadIdx.x; t < 256u; t += blockDim.x)
+        rb_sctab[t] = SinCosEntry{rb_sctab_src[2 * t], rb_sctab_src[2 * t + 1]};
     __syncthreads();
 }
 
@@ -498,6 +543,10 @@ RB_HD void sin_cos(double x, double &s, double &c) {
 }
 template <bool FAST>
 RB_HD void sin_cos(f2 x, f2 &s, f2 &c) {
+    if constexpr (FAST) {
+        sincos_hw(x, s, c);
+        return;
+    }
     float s0, c0, s1, c1;
     sin_cos<FAST>(x.x, s0, c0);
     sin_cos<FAST>(x.y, s1, c1);
@@ -520,6 +569,85 @@ __device__ __forceinline__ double recip(double x) {
     return r;
 }
 __device__ __forceinline__ f2 recip(f2 x) { return f2{__builtin_amdgcn_rcpf(x.x), __builtin_amdgcn_rcpf(x.y)}; }
+
+// ---------------------------------------------------------------------------- input guard
+// The batched kernels' input domain (include/rigidbody_batch.h "Input domain"): every input
+// finite and every revolute joint angle |q_j| < 2^41 rad (fp64) / 2^22 rad (fp32) -- inside the
+// exact range of each sincos reduction above.  A configuration outside it gets NaN in every
+// output.  The reference propagates NaN / Inf through its arithmetic (multibody.rs:111-174), but
+// the model-specialised kernels cannot lean on propagation: they compile under
+// -ffinite-math-only with the model's structural zeros folded, so FR3's torques, say, never
+// read q_0 (a rotation about the gravity axis) and a NaN there would leave them finite.  So the
+// kernels check, with arithmetic on an opaque zero z the compiler can neither fold nor reason
+// about: acc = sum_j v(x_j) z is +-0 while every input is finite and NaN once one is not;
+// angles are scaled by 2^128 / limit first, so |q| >= limit overflows to Inf.  Every output
+// leaves as y + acc.  The check runs in fp32 (one VGPR, half the issue cost of fp64): v(x) is x,
+// or for fp64 inputs the high word of x read as a float -- sign, the top 8 of the 11 exponent
+// bits, 23 mantissa bits -- which is Inf / NaN exactly when x's exponent is >= 0x7f8 (x is
+// NaN, Inf, or |x| >= 2^1017) and >= 2^6 exactly when |x| >= 2^41.  Cost per configuration:
+// one FMA per input, one more per angle, one add per output (packed pairs: v_pk for both).
+// On the host (the single-configuration ABI) angles are checked for Inf / NaN only: sincos_cw
+// falls back to the C library past 2^45, so every finite angle is in range there, as in the
+// reference.
+RB_HD float guard_view(float x) { return x; }
+RB_HD f2 guard_view(f2 x) { return x; }
+RB_HD float guard_view(double x) {
+    return __builtin_bit_cast(float, (uint32_t)(__builtin_bit_cast(uint64_t, x) >> 32));
+}
+RB_HD float angle_scale(double) { return 0x1p122f; }  // high word >= 2^6 (|q| >= 2^41) -> Inf
+RB_HD float angle_scale(float) { return 0x1p106f; }   // |q| >= 2^22 -> Inf
+RB_HD f2 angle_scale(f2) { return f2{0x1p106f, 0x1p106f}; }
+RB_HD float guard_acc(double) { return 0.0f; }
+RB_HD float guard_acc(float) { return 0.0f; }
+RB_HD f2 guard_acc(f2) { return f2{0.0f, 0.0f}; }
+
+template <typename T>
+struct InputGuard {
+    using A = decltype(guard_acc(T()));
+    A z, acc;
+    RB_HD InputGuard() : z(guard_acc(T())) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+        asm("" : "+s"(z));
+#endif
+        acc = z;
+    }
+    RB_HD void val(T x) { acc = fmadd(guard_view(x), z, acc); }
+    RB_HD void angle(T x) {
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+        acc = fmadd(guard_view(x) * angle_scale(x), z, acc);
+#else
+        val(x);
+#endif
+    }
+    template <int N>
+    RB_HD void vals(const T (&x)[N]) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) val(x[j]);
+    }
+    // joint positions: angles of revolute joints, displacements of prismatic ones
+    template <typename Topo, int N>
+    RB_HD void joints(const T (&q)[N]) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            if (Topo::prismatic(j))
+                val(q[j]);
+            else
+                angle(q[j]);
+        }
+    }
+    // fp32 outputs: y + acc.  fp64 outputs: the high word OR-ed with 0x7ff80000 (a quiet NaN
+    // whatever the rest) when acc is NaN -- one 32-bit integer op per output instead of an fp64
+    // add, and no fp64 copy of acc held across the backward sweep (fp64 FR3 pair: 127 instead
+    // of 129 VGPRs, the 4th wave per SIMD).  acc is +-0 or NaN: NaN iff (bits << 1) > 0xff000000.
+    RB_HD T out(T y) const {
+        if constexpr (__is_same(T, double)) {
+            const uint32_t m = (__builtin_bit_cast(uint32_t, acc) << 1) > 0xff000000u ? 0x7ff80000u : 0u;
+            return __builtin_bit_cast(T, __builtin_bit_cast(uint64_t, y) | ((uint64_t)m << 32));
+        } else {
+            return y + acc;
+        }
+    }
+};
 
 // Paired-lane row access: one configuration from each of two batch blocks.  Both halves
 // use the saddr form off ONE wave-uniform base (the pair's first block, element oA): the

@@ -87,7 +87,12 @@ RB_HD void force_to_parent(const M3<T> &E, const V3<T> &r, V3<T> &n, V3<T> &f) {
 // ----------------------------------------------------------------------------- RNEA
 template <typename T, int N, bool FAST, typename Topo, typename Out>
 RB_HD void rnea_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
-                                               const T (&qddv)[N], Out &&out) {
+                                               const T (&qddv)[N], Out &&out_) {
+    InputGuard<T> gd;  // out-of-domain configurations: NaN outputs (spatial.hip.hpp)
+    gd.template joints<Topo>(qv);
+    gd.vals(qdv);
+    gd.vals(qddv);
+    auto out = [&](int j, T v) { out_(j, gd.out(v)); };
     T cs[N], sn[N];
     V3<T> W[N], V[N], AW[N], AV[N];  // link velocity / acceleration (rot, lin), link coordinates
     V3<T> fn[N], ff[N];              // per-link spatial force (moment, force)
@@ -160,7 +165,12 @@ RB_HD void rnea_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N],
 // is written as exact zeros (as the serial kernel does).
 template <typename T, int N, bool FAST, typename Topo, typename Out>
 RB_HD void aba_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N], const T (&tv)[N],
-                                              Out &&out) {
+                                              Out &&out_) {
+    InputGuard<T> gd;  // out-of-domain configurations: NaN outputs (spatial.hip.hpp)
+    gd.template joints<Topo>(qv);
+    gd.vals(qdv);
+    gd.vals(tv);
+    auto out = [&](int j, T v) { out_(j, gd.out(v)); };
     T cs[N], sn[N];
     V3<T> W[N], V[N];                  // pass-1 velocities (read by children)
     T cw0[N], cw1[N], cv0[N], cv1[N];  // c_i = v_i x (S qd_i), nonzero entries
@@ -320,7 +330,10 @@ RB_HD void aba_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N], cons
 // Output as crba_body.hip.hpp: element row + N*col of the column-major matrix, upper
 // triangle; strictly-lower entries and non-ancestor pairs exact zeros.
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-RB_HD void crba_eval_tree(const T *mdl, const T (&qv)[N], Out &&out) {
+RB_HD void crba_eval_tree(const T *mdl, const T (&qv)[N], Out &&out_) {
+    InputGuard<T> gd;  // out-of-domain configurations: NaN upper triangle (spatial.hip.hpp)
+    gd.template joints<Topo>(qv);
+    auto out = [&](int e, T v) { out_(e, e % N <= e / N ? gd.out(v) : v); };
     T cs[N], sn[N];
     cfor<0, N>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
@@ -380,7 +393,10 @@ RB_HD void crba_eval_tree(const T *mdl, const T (&qv)[N], Out &&out) {
 // (multibody.rs:95-108, body Jacobian of the last link, rows [lin; rot], 6 x N column-major)
 // along the last link's ancestor path.
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-RB_HD void fwd_kin_tree(const T *mdl, const T (&qv)[N], Out &&out) {
+RB_HD void fwd_kin_tree(const T *mdl, const T (&qv)[N], Out &&out_) {
+    InputGuard<T> gd;  // out-of-domain configurations: NaN outputs (spatial.hip.hpp)
+    gd.template joints<Topo>(qv);
+    auto out = [&](int e, T v) { out_(e, gd.out(v)); };
     M3<T> R{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
     V3<T> p = v3(T(0), T(0), T(0));
     cfor<0, N>([&](auto jc) {
@@ -408,7 +424,10 @@ RB_HD void fwd_kin_tree(const T *mdl, const T (&qv)[N], Out &&out) {
 }
 
 template <typename T, int N, bool FAST, typename Topo, typename Out>
-RB_HD void jac_tree(const T *mdl, const T (&qv)[N], Out &&out) {
+RB_HD void jac_tree(const T *mdl, const T (&qv)[N], Out &&out_) {
+    InputGuard<T> gd;  // out-of-domain configurations: NaN outputs (spatial.hip.hpp)
+    gd.template joints<Topo>(qv);
+    auto out = [&](int e, T v) { out_(e, gd.out(v)); };
     // acc = pose of the last frame in frame i, leaf -> root, starting from the model tail
     // (the last link's axis-frame change, layout.hpp kTailOut)
     M3<T> R;

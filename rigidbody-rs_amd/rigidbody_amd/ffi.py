@@ -93,6 +93,8 @@ _sig("multibody_kernel_path_ex", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int,
 _sig("multibody_kernel_form_ex", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _i64, ctypes.c_int])
 _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
+_sig("multibody_jit_source_ex", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _i64, ctypes.c_int, ctypes.c_char_p, _i64])
+_sig("multibody_jit_compile_ex", _i64, [_vp, ctypes.c_int, ctypes.c_int, _i64, ctypes.c_int, ctypes.c_char_p])
 KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3, "fwd_kin": 4, "jac": 5}
 GENERAL_AXES, URDF_TREE, FLOATING_BASE = 1, 2, 4  # rigidbody_batch.h RB_MODEL_*
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -182,10 +184,12 @@ def _one_device(ts):
     return devs.pop()
 
 
-def _host_soa(arrs, n):
-    """[n, B] host arrays of one batched host call: same shape, n rows; float32 if every input
-    is float32 (the *_host_f32 entry points), float64 otherwise."""
-    dt = np.float32 if all(np.asarray(x).dtype == np.float32 for x in arrs) else np.float64
+def _host_soa(arrs, n, dtype):
+    """[n, B] host arrays of one batched host call: same shape, n rows, converted to `dtype`
+    (float64, the reference's Real, or float32 for the *_host_f32 entry points)."""
+    dt = np.dtype(dtype)
+    if dt not in (np.dtype(np.float64), np.dtype(np.float32)):
+        raise TypeError(f"dtype must be float64 or float32, got {dt}")
     out = [np.ascontiguousarray(x, dtype=dt) for x in arrs]
     for a in out:
         if a.ndim != 2 or a.shape[0] != n or a.shape != out[0].shape:
@@ -338,14 +342,20 @@ class Multibody:
     def rnea_kernel_path(self, f64=False) -> str:
         return self.kernel_path("rnea", f64)
 
-    def jit_source(self, f64=False, kind="rnea") -> str:
-        n = _lib.multibody_jit_source(self._h, KINDS[kind], int(bool(f64)), None, 0)
+    def jit_source(self, f64=False, kind="rnea", batch=1 << 20, tiled=False) -> str:
+        """hipRTC source of the kernel a launch of `batch` configurations takes (tiled: the
+        *_tiled entry points) -- multibody_jit_source_ex."""
+        k, f, b, t = KINDS[kind], int(bool(f64)), int(batch), int(bool(tiled))
+        n = _lib.multibody_jit_source_ex(self._h, k, f, b, t, None, 0)
+        if n < 0:
+            raise RigidBodyError(last_error())
         buf = ctypes.create_string_buffer(n + 1)
-        _lib.multibody_jit_source(self._h, KINDS[kind], int(bool(f64)), buf, n + 1)
+        _lib.multibody_jit_source_ex(self._h, k, f, b, t, buf, n + 1)
         return buf.value.decode()
 
-    def jit_compile(self, f64=False, arch="gfx950", kind="rnea") -> int:
-        r = _lib.multibody_jit_compile(self._h, KINDS[kind], int(bool(f64)), arch.encode())
+    def jit_compile(self, f64=False, arch="gfx950", kind="rnea", batch=1 << 20, tiled=False) -> int:
+        r = _lib.multibody_jit_compile_ex(self._h, KINDS[kind], int(bool(f64)), int(batch), int(bool(tiled)),
+                                          arch.encode())
         if r < 0:
             raise RigidBodyError(last_error())
         return r
@@ -528,16 +538,17 @@ class Multibody:
         return out
 
     # -------------------------------------------------------- batched, host [n, B]
-    def rnea_batch_host(self, q, qd, qdd):
-        """Blocking host form (multibody_rnea_batch_host_f32 / _f64 by the inputs' dtype)."""
-        return self._host_call("rnea", (q, qd, qdd))
+    def rnea_batch_host(self, q, qd, qdd, dtype=np.float64):
+        """Blocking host form: multibody_rnea_batch_host_f64 (default: fp64, the reference's Real,
+        whatever the inputs' dtype) or _f32 with dtype=np.float32."""
+        return self._host_call("rnea", (q, qd, qdd), dtype)
 
-    def fd_batch_host(self, q, qd, tau):
-        """Blocking host form (multibody_fd_batch_host_f32 / _f64 by the inputs' dtype)."""
-        return self._host_call("fd", (q, qd, tau))
+    def fd_batch_host(self, q, qd, tau, dtype=np.float64):
+        """Blocking host form: multibody_fd_batch_host_f64 (default) or _f32 (dtype=np.float32)."""
+        return self._host_call("fd", (q, qd, tau), dtype)
 
-    def _host_call(self, kind, ins):
-        arrs = _host_soa(ins, self.n)
+    def _host_call(self, kind, ins, dtype):
+        arrs = _host_soa(ins, self.n, dtype)
         B = arrs[0].shape[1]
         out = np.empty_like(arrs[0])
         f32 = arrs[0].dtype == np.float32

@@ -50,6 +50,12 @@ def test_gpus2_spawns_two_ranks(split):
         assert st["launches"] >= bench.SIDE_MIN_LAUNCHES
         assert len(st["per_rank"]) == 2 and all(r["steps"] == st["launches"] for r in st["per_rank"])
         assert st["global_batch"] == 1 << 20 and st["batch_per_gpu_max"] == 1 << 19
+        # SURVEY §8(d) config 4 (fp64 RNEA + FD on shards of one global 2^20 batch) beside it
+        c4 = line["secondary"]["strong_split_rnea_fd"]
+        assert c4["global_batch"] == bench.CONFIG4_BATCH and c4["batch_per_gpu_max"] == bench.CONFIG4_BATCH // 2
+        assert c4["launches"] >= bench.SIDE_MIN_LAUNCHES and len(c4["per_rank"]) == 2
+        assert c4["dtype"] == "f64" and c4["scaling"] == "strong" and "config 4" in c4["config"]
+    assert line["roofline_check"] == "ok"
 
 
 def test_single_rank_default():
@@ -131,6 +137,52 @@ def test_valu_roofline_from_committed_counters(workload, op, clock, dt, packed, 
     v = bench.valu_roofline(workload, op, clock, dt, 1 << 20, ms, packed)
     for k in ("issue_frac_2p4ghz", "issue_frac_held", "flop_frac"):
         assert 0 < v[k] <= 1.0, (k, v[k])
-    assert v["held_clock_ghz"] < 2.4 and v["flops_per_eval_ref"] > 1000
+    assert v["held_clock_ghz"] < 2.4 and v["kernel_tflops"] <= v["flop_peak_tflops"]
     per_inst = v["kernel_flops_per_eval"] / v["insts_per_eval"]
     assert 0.5 < per_inst < (4.5 if packed else 2.5), per_inst
+    # the reference formulation's operation count lives beside the roofline, not in it
+    assert not any(k.startswith("ref") or "flops_per_eval_ref" in k for k in v)
+    ref = bench.reference_formulation(op, 1 << 20, ms)
+    assert ref["flops_per_eval"] > 1000 and ref["flops_per_eval"] > v["kernel_flops_per_eval"]
+
+
+def _driver_lines():
+    """The committed driver-style bench lines (profiles/r0*/session*/bench_driver*.log)."""
+    import glob
+
+    out = []
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r0*", "session*", "bench_driver*.log"))):
+        for ln in open(path):
+            if ln.startswith("{") and '"metric"' in ln:
+                out.append((os.path.relpath(path, REPO), json.loads(ln)))
+    return out
+
+
+def test_roofline_block_consistent():
+    """Every *_frac in a bench line is in (0, 1] and no rate under roofline exceeds its peak
+    (bench.roofline_violations, which bench.py also writes into each line as roofline_check):
+    on synthetic lines that break each rule, and on the committed driver-style lines after the
+    reference formulation's rate is moved out of the roofline block as bench.py now does."""
+    sys.argv = ["bench.py"]
+    bench = pytest.importorskip("bench")
+    good = {"roofline": {"achieved": 5000.0, "peak": 8000.0, "frac": 0.625,
+                         "valu": {"issue_frac_held": 0.8, "kernel_tflops": 30.0, "flop_peak_tflops": 78.6}},
+            "secondary": {"x": {"hbm_frac": 0.5, "valu": {"flop_frac": 0.4}}}}
+    assert bench.roofline_violations(good) == []
+    for path, val in ((("roofline", "frac"), 1.2), (("roofline", "achieved"), 9000.0),
+                      (("roofline", "valu", "kernel_tflops"), 90.0), (("secondary", "x", "hbm_frac"), 0.0)):
+        bad = json.loads(json.dumps(good))
+        d = bad
+        for k in path[:-1]:
+            d = d[k]
+        d[path[-1]] = val
+        assert bench.roofline_violations(bad), path
+    lines = _driver_lines()
+    assert lines
+    for path, line in lines:
+        for v in [line.get("roofline", {}).get("valu", {})] + [s.get("valu", {}) for s in
+                                                               (line.get("secondary") or {}).values()
+                                                               if isinstance(s, dict)]:
+            for k in ("ref_equiv_tflops", "flops_per_eval_ref", "ref_source"):
+                (v or {}).pop(k, None)
+        assert bench.roofline_violations(line) == [], path

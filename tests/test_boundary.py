@@ -275,6 +275,32 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "rollout_lane2" not in c30.jit_source(False, "rollout")
     assert mb.jit_compile(f64=False, kind="rollout") > 1000
     assert "sctab_init" in mb.jit_source(True, "rnea") and "sctab_init" not in mb.jit_source(False, "rnea")
+    # the source of the kernel a given launch takes (multibody_jit_source_ex): the auto policy's
+    # form, tail and load / store policy per batch size and layout (capi.cpp jit_shape)
+    head = mb.jit_source(True, "rnea", batch=1 << 20, tiled=True)
+    assert "rnea_lane_seq2<" in head and "rnea_lane<" in head and "S_ =" in head  # pairs + one-per-lane tail
+    assert "rnea_lane_seq2<" in mb.jit_source(False, "rnea", batch=1 << 20, tiled=True)
+    assert "#define RB_NT 0" in mb.jit_source(False, "rnea", batch=1 << 20, tiled=True)
+    assert "#define RB_NT 3" in mb.jit_source(False, "rnea", batch=1 << 20, tiled=False)
+    assert "rnea_lane_seq2<" not in mb.jit_source(True, "rnea", batch=1 << 17)
+    assert "fdh_split_block1<" in mb.jit_source(False, "fd", batch=1 << 15)
+    assert "fdh_split_block2<" in mb.jit_source(False, "fd", batch=65536)
+    assert "fdh_split_block2<" in mb.jit_source(False, "fd", batch=1 << 17)
+    assert "fdh_lane2<" in mb.jit_source(False, "fd", batch=(1 << 17) + 1)
+    assert "rollout_split_block2<" in mb.jit_source(False, "rollout", batch=65536)
+    assert mb.jit_compile(f64=True, kind="rnea", batch=1 << 20, tiled=True) > 1000
+    # rnea_park (a production knob) is clamped to what 3 blocks per CU leave of the 160 KB LDS
+    # (8 links x 6 KB per block) instead of reaching hipRTC, which would fail and drop the launch
+    # to the generic kernel
+    assert "rnea_lane_park<T, N, true, 8>" in c30.jit_source(False, "rnea")
+    try:
+        ffi.set_tuning("rnea_park", 40)
+        assert "rnea_lane_park<T, N, true, 8>" in c30.jit_source(False, "rnea")
+        assert c30.jit_compile(f64=False, kind="rnea") > 1000
+        ffi.set_tuning("rnea_park", 5)
+        assert "rnea_lane_park<T, N, true, 5>" in c30.jit_source(False, "rnea")
+    finally:
+        ffi.set_tuning("rnea_park", -1)
     assert "RB_SPLIT_ROT 1" in mb.jit_source(False, "fd")  # FR3 frames are signed permutations
     try:
         for form, pack, marker in ((1, 2, "aba_lane2"), (1, 1, "aba_lane<"), (1, 3, "aba_lane_seq2<"),

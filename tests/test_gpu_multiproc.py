@@ -154,3 +154,11 @@ def test_bench_two_ranks_weak_with_strong_split():
     assert st["launches"] >= bench.SIDE_MIN_LAUNCHES
     assert [x["steps"] for x in st["per_rank"]] == [st["launches"]] * 2
     assert st["evals_per_s"] > 0 and "cpu_baseline" not in line
+    # SURVEY §8(d) config 4 in the N > 1 line: RNEA + FD fp64 on shards of one global 2^20 batch,
+    # both hipRTC kernels, its own budget, per-rank times
+    c4 = line["secondary"]["strong_split_rnea_fd"]
+    assert c4["kernel_path"] == "jit+jit" and c4["dtype"] == "f64"
+    assert c4["global_batch"] == bench.CONFIG4_BATCH and c4["batch_per_gpu_max"] == bench.CONFIG4_BATCH // 2
+    assert c4["launches"] >= bench.SIDE_MIN_LAUNCHES and [x["steps"] for x in c4["per_rank"]] == [c4["launches"]] * 2
+    assert c4["pairs_per_s"] > 0 and 0 < c4["hbm_frac_max_rank"] <= 1
+    assert line["roofline_check"] == "ok", line["roofline_check"]

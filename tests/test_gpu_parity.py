@@ -949,9 +949,11 @@ def test_host_batch_forms(ffi, dev, fr3_text, dtype):
     tdt = torch.float64 if dtype == "float64" else torch.float32
     x = {k: chains.host_uniform(7, B, *chains.input_ranges(lim, k), chains.SEED + 120 + i, dtype=dtype)
          for i, k in enumerate(("q", "qd", "qdd", "tau"))}
-    tau_h = mb.rnea_batch_host(x["q"], x["qd"], x["qdd"])
-    qdd_h = mb.fd_batch_host(x["q"], x["qd"], x["tau"])
+    tau_h = mb.rnea_batch_host(x["q"], x["qd"], x["qdd"], dtype=dtype)
+    qdd_h = mb.fd_batch_host(x["q"], x["qd"], x["tau"], dtype=dtype)
     assert tau_h.dtype == np.dtype(dtype) and qdd_h.dtype == np.dtype(dtype)
+    if dtype == "float32":  # fp32 inputs without dtype=: the fp64 entry point, as the reference
+        assert mb.rnea_batch_host(x["q"], x["qd"], x["qdd"]).dtype == np.float64
     t = {k: _t(v, dev, tdt) for k, v in x.items()}
     tau_d = mb.rnea_batch(t["q"], t["qd"], t["qdd"]).cpu().numpy()
     qdd_d = mb.fd_batch(t["q"], t["qd"], t["tau"]).cpu().numpy()

@@ -2,7 +2,9 @@
 hipcc for gfx950 with the same options, and report registers / occupancy and an
 instruction mix from the ISA.  CPU only (hipcc cross-compiles).
 
-usage: python tools/jit_audit.py KIND {f32,f64} [DOF]     KIND in rnea fd crba rollout
+usage: python tools/jit_audit.py KIND {f32,f64} [DOF] [--batch B] [--tiled]
+       KIND in rnea fd crba rollout fwd_kin jac; the kernel a launch of B configurations takes
+       (default 2^20, SoA), as multibody_jit_source_ex resolves it
 """
 import collections
 import os
@@ -17,11 +19,19 @@ CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rigidbody
 
 
 def main():
-    kind, dt = sys.argv[1], sys.argv[2]
-    dof = int(sys.argv[3]) if len(sys.argv) > 3 else 7
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kind")
+    ap.add_argument("dt", choices=["f32", "f64"])
+    ap.add_argument("dof", type=int, nargs="?", default=7)
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--tiled", action="store_true")
+    a = ap.parse_args()
+    kind, dt, dof = a.kind, a.dt, a.dof
     mb = ffi.Multibody.new() if dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(dof))
-    src = mb.jit_source(dt == "f64", kind)
-    d = f"/tmp/jit_audit_{kind}_{dt}_{dof}"
+    src = mb.jit_source(dt == "f64", kind, batch=a.batch, tiled=a.tiled)
+    d = f"/tmp/jit_audit_{kind}_{dt}_{dof}_{a.batch}{'_t' if a.tiled else ''}"
     os.makedirs(d, exist_ok=True)
     path = os.path.join(d, "k.hip")
     open(path, "w").write(src)
