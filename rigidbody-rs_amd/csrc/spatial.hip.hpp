@@ -455,6 +455,11 @@ constexpr float kInv2PiHi = 0x1.45f306p-3f, kInv2PiLo = 0x1.b93910p-28f;  // 1/2
 constexpr float kRevShifter = 0x1.8p23f;                                 // 1.5 * 2^23
 RB_HD void sincos_hw(float x, float &s, float &c) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr ((RB_VARIANT & 4096) != 0) {  // A/B only: the unreduced x * (1/2pi) of round 4
+        s = __builtin_amdgcn_sinf(x * kInv2PiHi);
+        c = __builtin_amdgcn_cosf(x * kInv2PiHi);
+        return;
+    }
     const float k = __builtin_fmaf(x, kInv2PiHi, kRevShifter) - kRevShifter;
     const float u = __builtin_fmaf(x, kInv2PiLo, __builtin_fmaf(x, kInv2PiHi, -k));
     s = __builtin_amdgcn_sinf(u);
@@ -465,6 +470,14 @@ RB_HD void sincos_hw(float x, float &s, float &c) {
 }
 RB_HD void sincos_hw(f2 x, f2 &s, f2 &c) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr ((RB_VARIANT & 4096) != 0) {
+        float s0, c0, s1, c1;
+        sincos_hw(x.x, s0, c0);
+        sincos_hw(x.y, s1, c1);
+        s = f2{s0, s1};
+        c = f2{c0, c1};
+        return;
+    }
     const f2 hi = f2{kInv2PiHi, kInv2PiHi}, lo = f2{kInv2PiLo, kInv2PiLo}, sh = f2{kRevShifter, kRevShifter};
     const f2 k = fmadd(x, hi, sh) - sh;
     const f2 u = fmadd(x, lo, fmadd(x, hi, -k));
@@ -520,9 +533,11 @@ __device__ __forceinline__ void sincos_tab(double x, double &s, double &c) {
     const double t = __builtin_fma(x, 4.074366543152521e+01, shifter);  // 128/pi
     const double k = t - shifter;
     const uint32_t ki = (uint32_t)__builtin_bit_cast(unsigned long long, t) & 255u;
+    // two-term Cody-Waite: pi/128 - (hi + mid) = -2.3e-35, which over the supported |x| < 2^41
+    // (|k| < 2^46.4, InputGuard) moves r by < 2.2e-21, 1/1000 of an ulp of r -- a third FMA
+    // with the lo term buys nothing there
     double r = __builtin_fma(-k, 2.454369260617026e-02, x);         // pi/128 hi
     r = __builtin_fma(-k, 9.567553118338697e-19, r);                 // pi/128 mid
-    r = __builtin_fma(-k, -2.3396639138424529e-35, r);               // pi/128 lo
     const SinCosEntry e = rb_sctab[ki];
     const double z = r * r;
     const double sr = __builtin_fma(r * z, __builtin_fma(z, 8.333291563954032e-03, -1.666666666647126e-01), r);
@@ -611,10 +626,14 @@ struct InputGuard {
 #endif
         acc = z;
     }
-    RB_HD void val(T x) { acc = fmadd(guard_view(x), z, acc); }
+    // RB_VARIANT bit 2048 (A/B only): no checks -- the round-4 kernels' arithmetic
+    static constexpr bool kOff = (RB_VARIANT & 2048) != 0;
+    RB_HD void val(T x) {
+        if constexpr (!kOff) acc = fmadd(guard_view(x), z, acc);
+    }
     RB_HD void angle(T x) {
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
-        acc = fmadd(guard_view(x) * angle_scale(x), z, acc);
+        if constexpr (!kOff) acc = fmadd(guard_view(x) * angle_scale(x), z, acc);
 #else
         val(x);
 #endif
@@ -640,7 +659,9 @@ struct InputGuard {
     // add, and no fp64 copy of acc held across the backward sweep (fp64 FR3 pair: 127 instead
     // of 129 VGPRs, the 4th wave per SIMD).  acc is +-0 or NaN: NaN iff (bits << 1) > 0xff000000.
     RB_HD T out(T y) const {
-        if constexpr (__is_same(T, double)) {
+        if constexpr (kOff) {
+            return y;
+        } else if constexpr (__is_same(T, double)) {
             const uint32_t m = (__builtin_bit_cast(uint32_t, acc) << 1) > 0xff000000u ? 0x7ff80000u : 0u;
             return __builtin_bit_cast(T, __builtin_bit_cast(uint64_t, y) | ((uint64_t)m << 32));
         } else {
