@@ -633,7 +633,8 @@ struct InputGuard {
     }
     RB_HD void angle(T x) {
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
-        if constexpr (!kOff) acc = fmadd(guard_view(x) * angle_scale(x), z, acc);
+        // bit 8192 (A/B only): no angle checks (rows the dynamics never read stay unread)
+        if constexpr (!kOff && (RB_VARIANT & 8192) == 0) acc = fmadd(guard_view(x) * angle_scale(x), z, acc);
 #else
         val(x);
 #endif
