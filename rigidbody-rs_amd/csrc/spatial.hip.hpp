@@ -369,7 +369,9 @@ RB_HD void reload_fence() { asm volatile("" ::: "memory"); }
 #ifndef RB_STAGE_MARKS
 #define RB_STAGE_MARKS 0
 #endif
-#if RB_STAGE_MARKS
+#if defined(RB_STAGE)
+// a host tool's own stage hook (tools/opcount.py)
+#elif RB_STAGE_MARKS
 #define RB_STAGE(name)                                       \
     do {                                                     \
         __builtin_amdgcn_sched_barrier(0);                   \

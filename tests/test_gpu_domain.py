@@ -408,3 +408,58 @@ def test_nonfinite_single_config_abi(ffi, dev, fr3_text):
                             assert (~np.isfinite(mb.jac_raw(x["q"]))).all(), (single_gpu, j, v)
     finally:
         ffi.set_tuning("single_gpu", 0)
+
+
+@pytest.mark.parametrize("case", ["tree9", "floating14"])
+def test_trees_domain(case, dev):
+    """Kinematic trees / a floating base (tree_body.hip.hpp): revolute angles
+    at |q| ~ 1e3 against the oracle's tree form (prismatic coordinates stay in their ranges -- a
+    displacement is not reduced), and NaN / Inf in any input of a configuration giving NaN in every
+    output of RNEA, forward dynamics, CRBA (upper triangle), fwd_kin and jac, fp64 and fp32."""
+    import test_gpu_tree as tt
+
+    mb, om = tt._setup(case)
+    n = mb.n
+    _, typ = mb.topology()
+    rev = typ == 0
+    B = 600
+    q, qd, qdd, tau = tt._inputs(mb, B, 77)
+    rng = np.random.default_rng(78)
+    q[rev] += rng.choice([-1.0, 1.0], (int(rev.sum()), B)) * 1e3
+    for dtype, tol in ((torch.float64, 1e-9), (torch.float32, 1e-4)):
+        npd = np.float64 if dtype == torch.float64 else np.float32
+        x = [a.astype(npd).astype(np.float64) for a in (q, qd, qdd, tau)]
+        t = [tt._t(a, dev, dtype) for a in x]
+        tau_g = mb.rnea_batch(t[0], t[1], t[2]).cpu().numpy().astype(np.float64)
+        ref = om.rnea_batch(x[0], x[1], x[2])
+        err = (np.abs(tau_g - ref).max(0) / (1 + np.abs(ref).max(0))).max()
+        assert err <= tol, (case, dtype, "rnea", err)
+        H = mb.crba_batch(t[0]).cpu().numpy().astype(np.float64)
+        errh = (np.abs(H - om.crba_batch(x[0])) / (1 + np.abs(om.crba_batch(x[0])))).max()
+        assert errh <= tol, (case, dtype, "crba", errh)
+        qdd_g = mb.fd_batch(t[0], t[1], t[3]).cpu().numpy().astype(np.float64)
+        res = om.rnea_batch(x[0], x[1], qdd_g) - x[3]
+        assert (np.abs(res) / (1 + np.abs(x[3]))).max() <= (1e-8 if dtype == torch.float64 else 1e-3), (case, dtype)
+        # non-finite inputs, one per column, every argument and joint
+        xp = [a.copy() for a in x]
+        cols = []
+        c = 0
+        for a in (0, 1, 2, 3):
+            for j in range(n):
+                xp[a][j, c] = [np.nan, np.inf, -np.inf][c % 3]
+                cols.append((a, c))
+                c += 1
+        tp = [tt._t(a, dev, dtype) for a in xp]
+        outs = {"rnea": (mb.rnea_batch(tp[0], tp[1], tp[2]), (0, 1, 2)),
+                "fd": (mb.fd_batch(tp[0], tp[1], tp[3]), (0, 1, 3)),
+                "crba": (mb.crba_batch(tp[0]), (0,)), "fwd_kin": (mb.fwd_kin_batch(tp[0]), (0,)),
+                "jac": (mb.jac_batch(tp[0]), (0,))}
+        upper = ~np.tril(np.ones((n, n)), -1).T.reshape(-1).astype(bool)
+        for name, (o, args) in outs.items():
+            o = o.cpu().numpy()
+            rows = upper if name == "crba" else np.ones(o.shape[0], bool)
+            for a, col in cols:
+                if a in args:
+                    assert (~np.isfinite(o[rows, col])).all(), (case, dtype, name, a, col)
+            clean = [col for col in range(c, B)]
+            assert np.isfinite(o[:, clean]).all(), (case, dtype, name)
