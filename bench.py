@@ -714,8 +714,8 @@ def _load_json(rel):
 
 def held_clock(name):
     """Median in-kernel shader clock (GHz) of kernel `name` under sustained load, from the
-    committed clock probe (tools/clock_probe.py, profiles/r04/clock_probe.jsonl), or None."""
-    path = os.path.join(REPO, "profiles", "r04", "clock_probe.jsonl")
+    committed clock probe (tools/clock_probe.py, profiles/r05/clock_probe.jsonl), or None."""
+    path = os.path.join(REPO, "profiles", "r05", "clock_probe.jsonl")
     if not os.path.exists(path):
         return None
     for ln in open(path):
@@ -757,7 +757,7 @@ def valu_roofline(workload, op_key, clock_key, dt_name, evals, kern_ms, packed):
         clk = held_clock(clock_key)
         if clk:
             out.update({"held_clock_ghz": clk, "issue_frac_held": busy / (clk * 1e9 * t),
-                        "clock_source": f"profiles/r04/clock_probe.jsonl [{clock_key}]"})
+                        "clock_source": f"profiles/r05/clock_probe.jsonl [{clock_key}]"})
         fl = tr.get("valu_flops_per_launch", {})
         # the SQ_INSTS_VALU_FLOPS_* counters count per wave-instruction (an FMA 2, a packed FMA 4):
         # x 64 lanes for the FLOPs executed, as rocprof-compute's VALU FLOP metric
@@ -881,7 +881,10 @@ def main(a):
                    "streams": a.streams, "split": a.split,
                    "batch_per_gpu": B, "global_batch": global_batch, "dof": n,
                    "parallelism": f"dp{world} ({a.split} split; independent shards, RCCL model broadcast)",
-                   "input_sets": r["sets"], "rotated_bytes": r["sets"] * r["bytes"], "kernel_path": kpath},
+                   "input_sets": r["sets"], "rotated_bytes": r["sets"] * r["bytes"], "kernel_path": kpath,
+                   "input_domain": ("every input of every configuration is read and checked (NaN / Inf / "
+                                    "|q| past 2^41 rad fp64, 2^22 fp32 -> NaN outputs; rigidbody_batch.h "
+                                    "'Input domain'), q_0 included, which FR3's torques do not depend on")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK,
                      "traffic": traffic["bytes_per_launch"] if traffic else None,

@@ -413,7 +413,7 @@ def test_nonfinite_single_config_abi(ffi, dev, fr3_text):
 @pytest.mark.parametrize("case", ["tree9", "floating14"])
 def test_trees_domain(case, dev):
     """Kinematic trees / a floating base (tree_body.hip.hpp): revolute angles
-    at |q| ~ 1e3 against the oracle's tree form (prismatic coordinates stay in their ranges -- a
+    moved by +-159 turns (|q| ~ 1e3) against the oracle's tree form (prismatic coordinates stay in their ranges -- a
     displacement is not reduced), and NaN / Inf in any input of a configuration giving NaN in every
     output of RNEA, forward dynamics, CRBA (upper triangle), fwd_kin and jac, fp64 and fp32."""
     import test_gpu_tree as tt
@@ -425,7 +425,9 @@ def test_trees_domain(case, dev):
     B = 600
     q, qd, qdd, tau = tt._inputs(mb, B, 77)
     rng = np.random.default_rng(78)
-    q[rev] += rng.choice([-1.0, 1.0], (int(rev.sum()), B)) * 1e3
+    # +-159 turns (~1e3 rad): the configuration, and so the conditioning of H (the floating base's
+    # pitch joint is singular at +-pi/2), stays the in-range one
+    q[rev] += rng.choice([-1.0, 1.0], (int(rev.sum()), B)) * (2 * math.pi * 159)
     for dtype, tol in ((torch.float64, 1e-9), (torch.float32, 1e-4)):
         npd = np.float64 if dtype == torch.float64 else np.float32
         x = [a.astype(npd).astype(np.float64) for a in (q, qd, qdd, tau)]
