@@ -932,10 +932,13 @@ def main(a):
             r4 = stub_measure(c4hi - c4lo, SIDE_MIN_LAUNCHES)
             k4 = "stub"
         else:
+            # eager C-ABI calls from Python are host-bound at ~7 us per 2^17 fp64 launch: the same
+            # launches replayed from a HIP graph give the device-bound rate beside them
             r4 = measure(mb, "rnea_fd", "f64", c4hi - c4lo, a.layout, None, 5, world, a.rotate_gib, chains.SEED,
-                         100.0, dev=dev)
+                         100.0, graph=True, dev=dev)
             k4 = "+".join(mb.kernel_path(k, True, c4hi - c4lo, a.layout == "tiled") for k in ("rnea", "fd"))
         w4, km4 = rdist.max_over_ranks([r4["wall"], r4["kernel_ms_avg"]], world, dev)
+        g4 = rdist.max_over_ranks([r4.get("graph_kernel_ms_avg", 0.0)], world, dev)[0]
         b4 = set_bytes(n, 1, 8, "rnea_fd")
         sec["strong_split_rnea_fd"] = {
             "config": "SURVEY §8(d) config 4: fr3 RNEA + forward dynamics, fp64, one global batch of "
@@ -943,10 +946,13 @@ def main(a):
             "pairs_per_s": cfg4 * r4["steps"] / w4, "global_batch": cfg4, "batch_per_gpu_max": -(-cfg4 // world),
             "launches": r4["steps"], "ms_per_step": w4 / r4["steps"] * 1e3, "kernel_ms_avg_max_rank": km4,
             "hbm_frac_max_rank": b4 * -(-cfg4 // world) / (km4 * 1e-3) / HBM_PEAK if not a.stub else None,
+            "graph_ms_per_step_max_rank": g4 if not a.stub else None,
+            "graph_pairs_per_s": cfg4 / (g4 * 1e-3) if (g4 and not a.stub) else None,
             "bytes_per_pair": b4, "kernel_path": k4, "dtype": "f64", "layout": a.layout,
             "per_rank": per_rank(r4, world, dev), "scaling": "strong",
             "timing": "own launch budget (bench.budget_steps; one step = the RNEA launch + the FD launch on "
-                      "the rank's shard), max over ranks",
+                      "the rank's shard), max over ranks; graph_*: the same launches replayed from a HIP graph "
+                      "on every rank (device-bound), max over ranks",
             "status": "measured by the driver's N > 1 runs; our 1-GPU leases cannot run it (DESIGN.md §6)"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.stub:
         line["cpu_baseline"] = cpu_baseline(n, a.kernel, a.cpu_seconds)

@@ -160,5 +160,5 @@ def test_bench_two_ranks_weak_with_strong_split():
     assert c4["kernel_path"] == "jit+jit" and c4["dtype"] == "f64"
     assert c4["global_batch"] == bench.CONFIG4_BATCH and c4["batch_per_gpu_max"] == bench.CONFIG4_BATCH // 2
     assert c4["launches"] >= bench.SIDE_MIN_LAUNCHES and [x["steps"] for x in c4["per_rank"]] == [c4["launches"]] * 2
-    assert c4["pairs_per_s"] > 0 and 0 < c4["hbm_frac_max_rank"] <= 1
+    assert c4["pairs_per_s"] > 0 and 0 < c4["hbm_frac_max_rank"] <= 1 and c4["graph_pairs_per_s"] > 0
     assert line["roofline_check"] == "ok", line["roofline_check"]
