@@ -198,7 +198,9 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // 131 instead of 125 VGPRs (3 waves/SIMD instead of 4), and all its grid forms (pairs,
     // single tail, one per lane below 2^19) must stay bit-identical to each other.
     const bool dyn = kind == JitKind::Rnea || kind == JitKind::Fd || kind == JitKind::Rollout;
-    const bool com = dyn && !(kind == JitKind::Rnea && f64) && !(tuning().jit_variant & 512);
+    // jit_variant bit 16384 (A/B): the centre-of-mass form for the fp64 RNEA too
+    const bool com = dyn && !(kind == JitKind::Rnea && f64 && !(tuning().jit_variant & 16384)) &&
+                     !(tuning().jit_variant & 512);
     // rnea_lane_park: fp32 one-per-lane RNEA of long serial chains in the centre-of-mass g-form
     // (signed-permutation frames), when the tuning asks for it
     // the parked forces take NP x 6 KB of LDS per 4-wave block: at most kMaxPark links, so that 3
@@ -288,6 +290,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // target (130 and 3 waves without): FR3 2^20 tiled 26.4 vs 27.0 us.
     int waves = jit_waves(kind, f64, m.n);
     if (fdh && pack == 2 && tuning().jit_waves < 0) waves = 4;
+    if (kind == JitKind::Rnea && f64 && (tuning().jit_variant & 32768) && tuning().jit_waves < 0) waves = 4;  // A/B
     if (const int w = waves)
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
     head_s += "void ";
