@@ -18,6 +18,7 @@ Prints ONE JSON line (rank 0).  See DESIGN.md §5 for how roofline/cpu_baseline 
 derived; profiles/ holds the rocprofv3 summaries these numbers are checked against.
 """
 import argparse
+import contextlib
 import ctypes
 import json
 import os
@@ -385,26 +386,44 @@ def q_launcher(mb, kernel, B, dtype, rotate_gib, seed=chains.SEED, layout="soa")
     return launch, per
 
 
-def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED):
-    """Closure issuing multibody_rollout_batch_* on one resident state (q, qd updated in
-    place by every launch) and a [K*n, B] torque sequence."""
+def _on_stream(sp):
+    """torch stream context for a raw stream pointer (the timing helpers pass torch's own)."""
+    cur = torch.cuda.current_stream()
+    if sp is None or (sp.value or 0) == cur.cuda_stream:
+        return contextlib.nullcontext()
+    return torch.cuda.stream(torch.cuda.ExternalStream(sp.value))
+
+
+def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED, reset=True, reset_only=False):
+    """Closure issuing multibody_rollout_batch_* (q, qd updated in place) on a [K*n, B] torque
+    sequence drawn within the effort limits.  reset=True (the bench's workload): every launch
+    first restores q, qd from the initial draw (one [2][n][B] device copy on the launch stream),
+    as an MPC iteration restarts its candidates from the measured state.  Without it the state
+    integrates launch after launch: random torques at the effort limits drive the light wrist
+    links past 1e3 rad/s within 50 launches (800 steps) and 95% of the configurations to Inf/NaN
+    within 200 (tools/roll_state.py, profiles/r05/roll_state.log) -- the timed region would run
+    on a diverged state.  reset_only=True issues the copy alone (its cost, reported beside)."""
     n = mb.n
-    q = torch.empty((n, B), dtype=dtype, device="cuda")
-    qd = torch.empty_like(q)
+    state = torch.empty((2, n, B), dtype=dtype, device="cuda")
+    q, qd = state[0], state[1]
     lim = mb.limits()
     ffi.fill_uniform(q, *chains.input_ranges(lim, "q"), seed)
     ffi.fill_uniform(qd, *chains.input_ranges(lim, "qd"), seed + 1)
+    init = state.clone()
     tau = torch.empty((K * n, B), dtype=dtype, device="cuda")
     lo, hi = chains.input_ranges(lim, "tau")
-    ffi.fill_uniform(tau, lo * K, hi * K, seed + 2)
+    ffi.fill_uniform(tau, lo * K, hi * K, seed + 2)  # list * K: the joints' ranges for every step row
     fn = getattr(ffi.lib(), f"multibody_rollout_batch_{'f32' if dtype == torch.float32 else 'f64'}")
     args = (mb.handle, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), dt, K, None, B, B)
 
     def launch(i, sp):
-        if fn(*args, sp):
+        if reset:
+            with _on_stream(sp):
+                state.copy_(init)
+        if not reset_only and fn(*args, sp):
             raise RuntimeError(ffi.last_error())
 
-    launch.keep = (q, qd, tau)
+    launch.keep = (q, qd, tau, init)
     return launch
 
 
@@ -553,11 +572,16 @@ def side_workloads(mb7, a):
     for dn, dt in (("f32", torch.float32), ("f64", torch.float64)):
         rl = rollout_launcher(mb7, a.batch, dt, K)
         nl = budget_steps(rl, lo=100)
-        w, km = time_launches(rl, nl, 3, 1, 300.0)
+        w, lm = time_launches(rl, nl, 3, 1, 300.0)
+        _, cm = time_launches(rollout_launcher(mb7, a.batch, dt, K, reset_only=True), nl, 3, 1, 0.0)
+        km = lm - cm
         sec[f"rollout_fr3_{dn}_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
-                                        "launches": nl,
+                                        "launches": nl, "launch_ms_avg": lm, "reset_ms_avg": cm,
                                         "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", dn == "f64"),
-                                        "note": "evals = configurations x Euler steps; q, qd stay on chip (LDS)",
+                                        "note": ("evals = configurations x Euler steps; q, qd stay on chip (LDS); "
+                                                 "every launch restarts from the initial state (a [2][n][B] device "
+                                                 "copy, reset_ms_avg, timed alone); evals_per_s includes it, "
+                                                 "kernel_ms_avg = launch_ms_avg - reset_ms_avg"),
                                         "valu": valu_roofline(f"rollout_fr3_{dn}_K16_b{a.batch}", "rollout_step_fr3",
                                                               f"rollout_fr3_{dn}", dn, a.batch * K, km, dn == "f32"),
                                         "reference_formulation": reference_formulation("rollout_step_fr3", a.batch * K, km)}
@@ -566,11 +590,14 @@ def side_workloads(mb7, a):
     Bs = 65536
     rl = rollout_launcher(mb7, Bs, torch.float32, K)
     nl = budget_steps(rl, lo=200)
-    w, km, gl = time_graph(rl, nl)
+    w, lm, gl = time_graph(rl, nl)
+    _, cm, _ = time_graph(rollout_launcher(mb7, Bs, torch.float32, K, reset_only=True), nl)
     sec["rollout_fr3_f32_K16_b65536_graph"] = {"steps_per_launch": K, "batch": Bs, "evals_per_s": Bs * K * gl / w,
-                                               "launches": gl, "kernel_ms_avg": km,
-                                               "launch": "HIP graph of 100 captured C-ABI launches, replayed",
-                                               "note": "evals = configurations x Euler steps"}
+                                               "launches": gl, "launch_ms_avg": lm, "reset_ms_avg": cm,
+                                               "kernel_ms_avg": lm - cm,
+                                               "launch": "HIP graph of 100 captured (reset copy + C-ABI launch) pairs, replayed",
+                                               "note": "evals = configurations x Euler steps; kernel_ms_avg = "
+                                                       "launch_ms_avg - reset_ms_avg (the copy's graph timed alone)"}
     return sec
 
 
