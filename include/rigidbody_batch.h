@@ -24,6 +24,11 @@
  * configuration at out[e * ld + b], with e following the single-call ABI's
  * column-major order (crba: e = row + n*col; jac: e = row + 6*col; fwd_kin: e = 0..2).
  *
+ * Batch size: any batch >= 0 (0 = nothing to do); one kernel launch covers at most 2^28
+ * configurations (lane byte offsets are 32-bit), larger batches are split into consecutive
+ * launches on the same stream (tests/test_gpu_limits.py: 2^28 + 257).  rb_fill_uniform_*
+ * alone takes at most 2^28 columns per call.
+ *
  * Pointers: the plain entry points take DEVICE pointers (hipMalloc'd memory on the
  * current HIP device) and enqueue asynchronously on `stream` (a hipStream_t; NULL =
  * the null stream).  The *_host variants take host pointers and block until done.
