@@ -162,3 +162,54 @@ def test_bench_two_ranks_weak_with_strong_split():
     assert c4["launches"] >= bench.SIDE_MIN_LAUNCHES and [x["steps"] for x in c4["per_rank"]] == [c4["launches"]] * 2
     assert c4["pairs_per_s"] > 0 and 0 < c4["hbm_frac_max_rank"] <= 1 and c4["graph_pairs_per_s"] > 0
     assert line["roofline_check"] == "ok", line["roofline_check"]
+
+
+RCCL_WORKER = textwrap.dedent('''
+    import os, sys, json
+    sys.path[:0] = [{repo!r}, {pkg!r}]
+    import numpy as np, torch, torch.distributed as dist
+    from rigidbody_amd import chains, ffi
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)   # RCCL, as bench.py at world > 1
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    mb0 = ffi.Multibody.new()
+    # the model broadcast of rigidbody_amd.dist.broadcast_model, on device tensors over RCCL
+    blob = torch.as_tensor(mb0.blob(), dtype=torch.float64, device=dev)
+    size = torch.tensor([blob.numel()], dtype=torch.int64, device=dev)
+    dist.broadcast(size, 0)
+    got = blob.clone()  # rank 0's buffer (the root of the broadcast)
+    dist.broadcast(got, 0)
+    mb = ffi.Multibody.from_blob(got.cpu().numpy())
+    mb.upload()
+    lim = mb.limits()
+    x = [ffi.fill_uniform(torch.empty((7, 4099), dtype=torch.float64, device=dev), *chains.input_ranges(lim, k),
+                          chains.SEED + i) for i, k in enumerate(("q", "qd", "qdd"))]
+    same = bool(torch.equal(mb.rnea_batch(*x), mb0.rnea_batch(*x)))
+    # the timing reductions of bench.py (max / gather over ranks) on device tensors
+    t = torch.tensor([1.5, 2.5], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    outs = [torch.zeros_like(t)]
+    dist.all_gather(outs, t)
+    dist.barrier()
+    torch.cuda.synchronize()
+    print(json.dumps({{"backend": dist.get_backend(), "blob_equal": bool(torch.equal(got, blob)),
+                      "rebuilt_bit_identical": same, "max": t.tolist(), "gather": outs[0].tolist()}}), flush=True)
+    dist.destroy_process_group()
+''')
+
+
+def test_rccl_process_group_world1(tmp_path):
+    """The RCCL ("nccl") process group of bench.py's N > 1 path, initialised on the box's one GPU
+    (RCCL takes one rank per device, so world 1 -- a 2-rank RCCL run needs two GPUs): the model
+    blob broadcast on device tensors, the Multibody rebuilt from it bit-identical on a batch, and
+    the max / gather reductions the timing uses."""
+    script = tmp_path / "rccl.py"
+    script.write_text(RCCL_WORKER.format(repo=REPO, pkg=PKG))
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, "-u", str(script)], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["backend"] == "nccl" and out["blob_equal"] and out["rebuilt_bit_identical"], out
+    assert out["max"] == [1.5, 2.5] and out["gather"] == [1.5, 2.5], out
