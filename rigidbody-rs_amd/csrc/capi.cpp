@@ -889,6 +889,9 @@ int multibody_topology(const Multibody *mb, int *parent, int *joint_type) {
     return RB_OK;
 }
 
+}  // extern "C"
+
+// C++ helpers of the kernel-inspection entry points below
 namespace {
 // The kernel a launch of `batch` configurations of `kind` takes: the same resolution as the
 // launchers (launch_*_any).  *generic = true when the precompiled kernel runs (serial revolute
@@ -933,6 +936,8 @@ void note_jit_errors(const Multibody *mb) {
         if (!kv.second.error.empty()) g_last_error = kv.second.error;
 }
 }  // namespace
+
+extern "C" {
 
 int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled) {
     if (int rc = check_kernel_query(mb, kind, batch)) return -rc;
