@@ -68,9 +68,8 @@ int jit_waves(JitKind kind, bool f64, int n) {
     const int v = tuning().jit_waves;
     if (v >= 0) return v;
     if (kind == JitKind::Rollout && !f64 && n <= 8) return jit_pack(kind, f64, n) != 1 ? 2 : 4;
-    // fp64 short-chain rollout: 126 VGPRs at the target, 129 (3 waves/SIMD) without it since the
-    // input checks (InputGuard, spatial.hip.hpp)
-    if (kind == JitKind::Rollout && f64 && n <= 8) return 4;
+    // (the fp64 rollout of the mass-matrix form takes a 4-wave target in jit_source; the ABA
+    // form -- the rollout of trees, or fd_form 1 -- none: 436 B of scratch per lane under it)
     return 0;
 }
 
@@ -290,6 +289,13 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // target (130 and 3 waves without): FR3 2^20 tiled 26.4 vs 27.0 us.
     int waves = jit_waves(kind, f64, m.n);
     if (fdh && pack == 2 && tuning().jit_waves < 0) waves = 4;
+    // fp64 rollout of the mass-matrix form: 127 VGPRs, 4 waves/SIMD either way since the input
+    // checks; the target keeps it there (FR3 2^20 x 16 steps, reset state: 690-708 vs 702-704 us,
+    // noise-level).  Not for the ABA form: 256 VGPRs at 1 wave/SIMD runs 984 us, 2 / 3 / 4-wave
+    // targets spill (1068 / 2756 / 4131 us; profiles/r05/ab/rollout_forms/).
+    if (kind == JitKind::Rollout && f64 && m.n <= 8 && jit_fd_form(m) == 2 && !(tuning().jit_variant & 256) &&
+        tuning().jit_waves < 0)
+        waves = 4;
     if (kind == JitKind::Rnea && f64 && (tuning().jit_variant & 32768) && tuning().jit_waves < 0) waves = 4;  // A/B
     if (const int w = waves)
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
