@@ -133,7 +133,8 @@ std::string jit_tag(JitKind kind, bool f64, int n) {
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n)) +
            ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":r" + std::to_string(tuning().split_rot) + ":v" +
            std::to_string(tuning().jit_variant) + ":f" + std::to_string(tuning().fd_form) + ":k" +
-           std::to_string(kind == JitKind::Rnea ? tuning().rnea_park.load() : 0);
+           std::to_string(kind == JitKind::Rnea ? tuning().rnea_park.load() : 0) + ":e" +
+           std::to_string(kind == JitKind::Rnea ? tuning().rnea_rev.load() : 0);
 }
 
 std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req, int tail, int nt) {
@@ -198,7 +199,12 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // single tail, one per lane below 2^19) must stay bit-identical to each other.
     const bool dyn = kind == JitKind::Rnea || kind == JitKind::Fd || kind == JitKind::Rollout;
     // jit_variant bit 16384 (A/B): the centre-of-mass form for the fp64 RNEA too
-    const bool com = dyn && !(kind == JitKind::Rnea && f64 && !(tuning().jit_variant & 16384)) &&
+    // rnea_lane_rev: the fp64 RNEA of serial chains longer than 8 links, whose per-link forces
+    // hold one wave per SIMD (12 links 264 VGPRs, 30 links 496) and do not fit LDS either
+    // (rnea_park's fp64 forces would take 60 KB per wave); centre-of-mass g-form, signed-permutation
+    // frames (checked with the kernel form below)
+    const bool rev = kind == JitKind::Rnea && f64 && m.n > 8 && m.serial_revolute() && tuning().rnea_rev != 0;
+    const bool com = dyn && !(kind == JitKind::Rnea && f64 && !rev && !(tuning().jit_variant & 16384)) &&
                      !(tuning().jit_variant & 512);
     // rnea_lane_park: fp32 one-per-lane RNEA of long serial chains in the centre-of-mass g-form
     // (signed-permutation frames), when the tuning asks for it
@@ -325,6 +331,13 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << seq_prologue;
         o << "  rbamd::dev::rnea_lane_seq2<T, N, " << F
           << ", Topo>(kModel, q + oA, qd + oA, qdd + oA, tau + oA, offA, offB, twoB, ld);\n}\n";
+    } else if (kind == JitKind::Rnea && rev && com && (sr > 0 || (sr < 0 && perm)) && pack == 1) {
+        o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+             "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+        o << "  rbamd::dev::rnea_lane_rev<T, N, " << F << ">(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n}\n";
     } else if (kind == JitKind::Rnea && park > 0) {
         o << "extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void "
              "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "

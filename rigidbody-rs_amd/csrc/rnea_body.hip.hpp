@@ -290,6 +290,112 @@ __device__ __forceinline__ void rnea_lane_park(const T *mdl, const T *__restrict
     st_row(tau, 0, off, n.z);
 }
 
+// Reversed-sweep form of long serial chains (fp64; jit.cpp): no per-link storage.  The forward
+// sweep (multibody.rs:122-141) carries only the link kinematics (w, v, aw, av) to the leaf; the
+// backward sweep (143-150) walks back from the leaf, each step forming link j's wrench from its
+// kinematics (link_force_g), adding the child's transmitted wrench, and recovering link j-1's
+// kinematics by inverting the forward step with the reloaded (q_j, qd_j, qdd_j) -- E_j is
+// orthonormal, so
+//   w_{j-1}  = E (w_j - qd z)                 aw_{j-1} = E (aw_j - qdd z - w_j x qd z)
+//   v_{j-1}  = E v_j + p x w_{j-1}            av_{j-1} = E (av_j - v_j x qd z) + p x aw_{j-1}.
+// Live set: the 12 kinematic values, the 6 of the transmitted wrench and the rows in flight,
+// where rnea_eval holds (n, g) and (cos, sin) per link (fp64, 30 links: ~500 VGPRs, one wave per
+// SIMD; parking them in LDS as rnea_lane_park does would need 60 KB per wave).  The kinematics
+// are evaluated twice (once each way), sincos twice, and the rows are read twice (the second read
+// mostly from the Infinity Cache); the recovered kinematics carry a few extra roundings per link.
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void rnea_lane_rev(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                              const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b,
+                                              int64_t ld) {
+    static_assert(kRneaGForm, "centre-of-mass g-form serial chains only");
+    constexpr int PF = 4, PB = 4;  // load distance (links) of the forward / backward sweep
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    T qv[N], qdv[N], qddv[N];
+    auto load = [&](int j) {  // temporal: the backward sweep reads the rows again
+        qv[j] = ld_row<T, false>(q, j * ld, off);
+        qdv[j] = ld_row<T, false>(qd, j * ld, off);
+        qddv[j] = ld_row<T, false>(qdd, j * ld, off);
+    };
+#pragma unroll
+    for (int j = 0; j < PF && j < N; ++j) load(j);
+    InputGuard<T> gd;  // out-of-domain configurations: NaN torques (spatial.hip.hpp)
+    RneaState<T> st;
+    {  // link 0's kinematics (rnea_fwd0; its wrench is formed in the backward sweep)
+        T sn, cs;
+        gd.angle(qv[0]);
+        gd.val(qdv[0]);
+        gd.val(qddv[0]);
+        sin_cos<FAST>(qv[0], sn, cs);
+        const M3<T> E = joint_rotation(load_link(mdl, 0).Rp, cs, sn);
+        const T g = T(kGravity);
+        st.w = v3(T(0), T(0), RB_GUARD_ANCHOR ? gd.out(qdv[0]) : qdv[0]);
+        st.v = v3(T(0), T(0), T(0));
+        st.aw = v3(T(0), T(0), qddv[0]);
+        st.av = v3(g * E.m[6], g * E.m[7], g * E.m[8]);
+    }
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+        if (j + PF - 1 < N) load(j + PF - 1);
+        const Link<T> L = load_link(mdl, j);
+        const T qj = qv[j], qdj = qdv[j], qddj = qddv[j];
+        gd.angle(qj);
+        gd.val(qdj);
+        gd.val(qddj);
+        T sn, cs;
+        sin_cos<FAST>(qj, sn, cs);
+        const M3<T> E = joint_rotation(L.Rp, cs, sn);
+        const V3<T> u = cross_sub(st.v, L.p, st.w);
+        const V3<T> ua = cross_sub(st.av, L.p, st.aw);
+        V3<T> wn = mul_t(E, st.w), vn = mul_t(E, u);
+        V3<T> awn = mul_t(E, st.aw), avn = mul_t(E, ua);
+        wn.z += qdj;
+        if constexpr (RB_GUARD_ANCHOR != 0) wn.z = gd.out(wn.z);
+        awn.z += qddj;
+        avn.x = fmadd(vn.y, qdj, avn.x);
+        avn.y = fmadd(-vn.x, qdj, avn.y);
+        awn.x = fmadd(wn.y, qdj, awn.x);
+        awn.y = fmadd(-wn.x, qdj, awn.y);
+        st.w = wn; st.v = vn; st.aw = awn; st.av = avn;
+        __builtin_amdgcn_sched_barrier(0);  // keeps the loads PF links ahead, not all hoisted
+    }
+    reload_fence();
+    // backward sweep: rows reloaded PB links ahead, leaf first
+#pragma unroll
+    for (int j = N - 1; j >= N - PB && j >= 0; --j) load(j);
+    V3<T> F, n;  // the wrench link j transmits to its parent, in link j's frame
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) {
+        if (j - PB >= 0) load(j - PB);
+        const Link<T> L = load_link(mdl, j);
+        V3<T> fn, gg;
+        link_force_g(L, j, st.w, st.v, st.aw, st.av, fn, gg);
+        if (j == N - 1) {
+            poison_leaf(gd, fn, gg);  // as rnea_eval: a NaN wrench reaches every parent
+            F = v3(L.m * gg.x, L.m * gg.y, L.m * gg.z);
+            n = fn;
+        } else {
+            F = v3(fmadd(L.m, gg.x, F.x), fmadd(L.m, gg.y, F.y), fmadd(L.m, gg.z, F.z));
+            n = v3(fn.x + n.x, fn.y + n.y, fn.z + n.z);
+        }
+        st_row(tau, j * ld, off, n.z);
+        if (j == 0) break;
+        T s, c;
+        sin_cos<FAST>(qv[j], s, c);
+        const M3<T> E = joint_rotation(L.Rp, c, s);
+        const T qdj = qdv[j], qddj = qddv[j];
+        const V3<T> fl = mul(E, F);  // the parent's share: E F and E n + p x (E F)
+        n = cross_add(mul(E, n), L.p, fl);
+        F = fl;
+        const V3<T> wp = mul(E, v3(st.w.x, st.w.y, st.w.z - qdj));
+        const V3<T> awp = mul(E, v3(fmadd(-st.w.y, qdj, st.aw.x), fmadd(st.w.x, qdj, st.aw.y), st.aw.z - qddj));
+        const V3<T> vp = cross_add(mul(E, st.v), L.p, wp);
+        const V3<T> avp = cross_add(mul(E, v3(fmadd(-st.v.y, qdj, st.av.x), fmadd(st.v.x, qdj, st.av.y), st.av.z)),
+                                    L.p, awp);
+        st.w = wp; st.v = vp; st.aw = awp; st.av = avp;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Streaming form (precompiled generic kernels, rnea.hip): walk the batch with `stride`,
 // prefetching the next configuration's joint values into registers before evaluating the
 // current one.

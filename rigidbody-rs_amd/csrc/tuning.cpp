@@ -39,6 +39,7 @@ const Key kKeys[] = {
     {"single_gpu", &Tuning::single_gpu, false},
     {"fd_form", &Tuning::fd_form, false},
     {"rnea_park", &Tuning::rnea_park, false},
+    {"rnea_rev", &Tuning::rnea_rev, false},
     {"grid_factor", &Tuning::grid_factor, true},
     {"rnea_nt", &Tuning::rnea_nt, true},
     {"fd_nt", &Tuning::fd_nt, true},

@@ -1,7 +1,7 @@
 // tuning.hpp -- launch-shape knobs (host side) and resident-grid sizing.
 //
 // Production knobs (rb_set_tuning accepts these always): `jit`, `pack`, `rnea_stream`,
-// `single_gpu`, `fd_form`, `rnea_park`.
+// `single_gpu`, `fd_form`, `rnea_park`, `rnea_rev`.
 // Everything else is an A/B experiment selector: rb_set_tuning accepts it only when the
 // process runs with RB_EXPERIMENTAL=1 (tools/ab_bench.py, tools/small_batch.py), so a normal
 // caller cannot multiply the hipRTC kernel variants (jit.cpp cache key) or the test matrix.
@@ -42,6 +42,11 @@ struct Tuning {
     // instead of 2; 0 = off, -1 auto (8 for chains of 20+ links: 30-link 2^20 91.0 vs 103.4 us,
     // bit-identical).
     std::atomic<int> rnea_park{-1};
+    // JIT fp64 RNEA of serial chains longer than 8 links: the reversed-sweep form
+    // (rnea_body.hip.hpp rnea_lane_rev: the backward sweep recovers each parent's kinematics by
+    // inverting the forward step, no per-link storage, 3-5 waves/SIMD instead of 1); 0 = off,
+    // 1 = on, -1 auto = on (12 links 2^20 tiled: 80.3 vs 107.6 us, 30 links 249 vs 328).
+    std::atomic<int> rnea_rev{-1};
 
     // ---- experimental (RB_EXPERIMENTAL=1)
     std::atomic<int> grid_factor{1};  // streaming grid = grid_factor x resident blocks (capped by the batch)
