@@ -269,7 +269,12 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "fdh_lane" not in c30.jit_source(False, "fd")        # ... the ABA for 30 links
     assert "rnea_lane<" in mb.jit_source(False, "rnea")         # fp32 RNEA one per lane
     assert "rnea_lane_seq2<" in mb.jit_source(True, "rnea")     # fp64 RNEA: sequential pair
-    assert "rnea_lane<" in c30.jit_source(True, "rnea")         # ... up to 8 links
+    assert "rnea_lane_rev<" in c30.jit_source(True, "rnea")     # ... up to 8 links; longer: reversed sweep
+    try:
+        ffi.set_tuning("rnea_rev", 0)
+        assert "rnea_lane<" in c30.jit_source(True, "rnea")     # stored-force form on request
+    finally:
+        ffi.set_tuning("rnea_rev", -1)
     assert "rollout_lane2" in mb.jit_source(False, "rollout")   # paired fp32 rollout
     assert "rollout_lane2" not in mb.jit_source(True, "rollout")
     assert "rollout_lane2" not in c30.jit_source(False, "rollout")
