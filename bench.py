@@ -546,6 +546,7 @@ def side_workloads(mb7, a):
     mb30 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(30))
     mb30.upload()
     one("rnea_chain30_f32", mb30, "rnea", "f32")             # config 5
+    one("rnea_chain30_f64", mb30, "rnea", "f64")             # the same chain in the reference's Real
     # a floating-base branching tree (6 virtual + 8 joints, 2 prismatic)
     mbt = ffi.Multibody.from_urdf_string(chains.tree_urdf(floating=True), ffi.FLOATING_BASE)
     mbt.upload()
