@@ -201,8 +201,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // jit_variant bit 16384 (A/B): the centre-of-mass form for the fp64 RNEA too
     // rnea_lane_rev: the fp64 RNEA of serial chains longer than 8 links, whose per-link forces
     // hold one wave per SIMD (12 links 264 VGPRs, 30 links 496) and do not fit LDS either
-    // (rnea_park's fp64 forces would take 60 KB per wave); centre-of-mass g-form, signed-permutation
-    // frames (checked with the kernel form below)
+    // (rnea_park's fp64 forces would take 60 KB per wave); centre-of-mass link forces, any joint
+    // frames (general axes included)
     const bool rev = kind == JitKind::Rnea && f64 && m.n > 8 && m.serial_revolute() && tuning().rnea_rev != 0;
     const bool com = dyn && !(kind == JitKind::Rnea && f64 && !rev && !(tuning().jit_variant & 16384)) &&
                      !(tuning().jit_variant & 512);
@@ -331,7 +331,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << seq_prologue;
         o << "  rbamd::dev::rnea_lane_seq2<T, N, " << F
           << ", Topo>(kModel, q + oA, qd + oA, qdd + oA, tau + oA, offA, offB, twoB, ld);\n}\n";
-    } else if (kind == JitKind::Rnea && rev && com && (sr > 0 || (sr < 0 && perm)) && pack == 1) {
+    } else if (kind == JitKind::Rnea && rev && com && pack == 1) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, T *__restrict__ tau, uint32_t B, int64_t ld, int64_t bs) {\n";
         o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";

@@ -307,7 +307,7 @@ template <typename T, int N, bool FAST>
 __device__ __forceinline__ void rnea_lane_rev(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
                                               const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b,
                                               int64_t ld) {
-    static_assert(kRneaGForm, "centre-of-mass g-form serial chains only");
+    static_assert(RB_COM_FORM != 0, "centre-of-mass link forces (link_force_g) only");
     constexpr int PF = 4, PB = 4;  // load distance (links) of the forward / backward sweep
     const uint32_t off = b * (uint32_t)sizeof(T);
     T qv[N], qdv[N], qddv[N];

@@ -21,10 +21,14 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _setup(n):
+def _setup(n, general=False):
     from oracle import oracle, urdf_model
     from rigidbody_amd import chains, ffi
 
+    if general:  # general joint axes (dense joint frames, RB_SPLIT_ROT off), as test_gpu_general
+        xml = chains.general_chain_urdf(n)
+        return (ffi, chains, ffi.Multibody.from_urdf_string(xml, ffi.URDF_TREE | ffi.GENERAL_AXES),
+                oracle.Model(frames=urdf_model.model_frames_from_urdf_tree(xml), general=True))
     xml = chains.synthetic_chain_urdf(n)
     return ffi, chains, ffi.Multibody.from_urdf_string(xml), oracle.Model(urdf_model.model_raw_from_urdf(xml))
 
@@ -40,10 +44,11 @@ def _rnea(ffi, mb, x, tiled, rev):
         ffi.set_tuning("rnea_rev", -1)
 
 
-@pytest.mark.parametrize("n", [12, 30])
-def test_rev_f64_vs_oracle_and_stored_form(n, dev):
-    ffi, chains, mb, om = _setup(n)
+@pytest.mark.parametrize("n,general", [(12, False), (30, False), (12, True)])
+def test_rev_f64_vs_oracle_and_stored_form(n, general, dev):
+    ffi, chains, mb, om = _setup(n, general)
     assert mb.kernel_path("rnea", True) == "jit"
+    assert "rnea_lane_rev<" in mb.jit_source(True, "rnea")
     lim = mb.limits()
     for B in (1, 63, 1000, 65536 + 77, 1 << 20):
         x = [ffi.fill_uniform(torch.empty((n, B), dtype=torch.float64, device=dev), *chains.input_ranges(lim, k),
