@@ -4,6 +4,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <string_view>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -129,7 +130,9 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
 }
 
 std::string jit_tag(JitKind kind, bool f64, int n) {
-    return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":o" +
+    // ":w" the policy's target, ":W" the raw knob (-1 lets jit_compile rebuild at the occupancy cliff)
+    return ":nt" + std::to_string(jit_nt(kind)) + ":w" + std::to_string(jit_waves(kind, f64, n)) + ":W" +
+           std::to_string(tuning().jit_waves.load()) + ":o" +
            std::to_string(jit_opaque(kind, f64, n) ? 1 : 0) + ":p" + std::to_string(jit_pack(kind, f64, n)) +
            ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":r" + std::to_string(tuning().split_rot) + ":v" +
            std::to_string(tuning().jit_variant) + ":f" + std::to_string(tuning().fd_form) + ":k" +
@@ -137,7 +140,23 @@ std::string jit_tag(JitKind kind, bool f64, int n) {
            std::to_string(kind == JitKind::Rnea ? tuning().rnea_rev.load() : 0);
 }
 
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req, int tail, int nt) {
+int code_vgprs(const std::vector<char> &code) {
+    // msgpack map entry ".vgpr_count" (fixstr 0xab) -> positive fixint / uint8 (0xcc) / uint16 (0xcd)
+    static const char key[] = "\xab.vgpr_count";
+    const std::string_view buf(code.data(), code.size());
+    const size_t at = buf.find(std::string_view(key, sizeof(key) - 1));
+    if (at == std::string_view::npos) return -1;
+    size_t i = at + sizeof(key) - 1;
+    if (i >= buf.size()) return -1;
+    const unsigned char t = (unsigned char)buf[i];
+    if (t < 0x80) return t;
+    if (t == 0xcc && i + 1 < buf.size()) return (unsigned char)buf[i + 1];
+    if (t == 0xcd && i + 2 < buf.size()) return ((unsigned char)buf[i + 1] << 8) | (unsigned char)buf[i + 2];
+    return -1;
+}
+
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack_req, int tail, int nt,
+                       int waves_req) {
     std::vector<double> pk = m.pack_f64();
     for (int i = 0; i < m.n; ++i) {
         double *c = &pk[(size_t)i * kLinkStride];
@@ -293,16 +312,17 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     std::string head_s = "extern \"C\" __global__ __launch_bounds__(256) ";
     // The paired mass-matrix FD fits 4 waves/SIMD at exactly 128 VGPRs with the occupancy
     // target (130 and 3 waves without): FR3 2^20 tiled 26.4 vs 27.0 us.
-    int waves = jit_waves(kind, f64, m.n);
-    if (fdh && pack == 2 && tuning().jit_waves < 0) waves = 4;
+    int waves = waves_req >= 0 ? waves_req : jit_waves(kind, f64, m.n);
+    if (fdh && pack == 2 && tuning().jit_waves < 0 && waves_req < 0) waves = 4;
     // fp64 rollout of the mass-matrix form: 127 VGPRs, 4 waves/SIMD either way since the input
     // checks; the target keeps it there (FR3 2^20 x 16 steps, reset state: 690-708 vs 702-704 us,
     // noise-level).  Not for the ABA form: 256 VGPRs at 1 wave/SIMD runs 984 us, 2 / 3 / 4-wave
     // targets spill (1068 / 2756 / 4131 us; profiles/r05/ab/rollout_forms/).
     if (kind == JitKind::Rollout && f64 && m.n <= 8 && jit_fd_form(m) == 2 && !(tuning().jit_variant & 256) &&
-        tuning().jit_waves < 0)
+        tuning().jit_waves < 0 && waves_req < 0)
         waves = 4;
-    if (kind == JitKind::Rnea && f64 && (tuning().jit_variant & 32768) && tuning().jit_waves < 0) waves = 4;  // A/B
+    if (kind == JitKind::Rnea && f64 && (tuning().jit_variant & 32768) && tuning().jit_waves < 0 && waves_req < 0)
+        waves = 4;  // A/B
     if (const int w = waves)
         head_s += "__attribute__((amdgpu_waves_per_eu(" + std::to_string(w) + "))) ";
     head_s += "void ";
@@ -428,9 +448,9 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     return src;
 }
 
-bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
-                 std::vector<char> *code, std::string *error, int pack, int tail, int nt) {
-    const std::string src = jit_source(m, kind, f64, fast, pack, tail, nt);
+namespace {
+bool rtc_compile(const std::string &src, const std::string &arch, bool no_licm, std::vector<char> *code,
+                 std::string *error) {
     hiprtcProgram prog = nullptr;
     if (hiprtcCreateProgram(&prog, src.c_str(), "rb_jit.hip", kJitHeaderCount, kJitHeaderSources,
                             kJitHeaderNames) != HIPRTC_SUCCESS) {
@@ -440,10 +460,7 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     const std::string arch_opt = "--offload-arch=" + arch;
     const char *opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffinite-math-only", "-fno-signed-zeros"};
     std::vector<const char *> optv(opts, opts + sizeof(opts) / sizeof(opts[0]));
-    // The paired fp32 rollout and the fp64 rollout of short chains keep 2 waves/SIMD only
-    // without machine LICM: hoisting per-step address arithmetic and constants out of the K
-    // loop costs the VGPRs below 256 (fp64 FR3: 212 instead of 264).
-    if (kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack > 0 ? pack : jit_pack(kind, f64, m.n))) {
+    if (no_licm) {
         optv.push_back("-mllvm");
         optv.push_back("-disable-machine-licm");
     }
@@ -462,6 +479,31 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
     code->resize(code_size);
     hiprtcGetCode(prog, code->data());
     hiprtcDestroyProgram(&prog);
+    return true;
+}
+}  // namespace
+
+bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
+                 std::vector<char> *code, std::string *error, int pack, int tail, int nt) {
+    std::string src = jit_source(m, kind, f64, fast, pack, tail, nt);
+    // The paired fp32 rollout and the fp64 rollout of short chains keep 2 waves/SIMD only
+    // without machine LICM: hoisting per-step address arithmetic and constants out of the K
+    // loop costs the VGPRs below 256 (fp64 FR3: 212 instead of 264).
+    const bool no_licm = kind == JitKind::Rollout && jit_rollout_no_hoist(f64, m.n, pack > 0 ? pack : jit_pack(kind, f64, m.n));
+    if (!rtc_compile(src, arch, no_licm, code, error)) return false;
+    // Occupancy cliff (jit.hpp): no target asked for, none in the source, and the kernel just
+    // past 256 registers -> rebuild with a 2-wave target; the first build stands if that fails.
+    if (tuning().jit_waves < 0 && src.find("amdgpu_waves_per_eu") == std::string::npos) {
+        const int v = code_vgprs(*code);
+        if (v > 256 && v <= 272) {
+            std::string src2 = jit_source(m, kind, f64, fast, pack, tail, nt, 2), err2;
+            std::vector<char> code2;
+            if (rtc_compile(src2, arch, no_licm, &code2, &err2)) {
+                code->swap(code2);
+                src.swap(src2);
+            }
+        }
+    }
     // RB_JIT_DUMP=dir: keep every compiled source and code object for inspection
     // (llvm-objdump / llvm-readelf on the .co: registers, scratch, ISA of what really runs)
     if (const char *dir = std::getenv("RB_JIT_DUMP")) {

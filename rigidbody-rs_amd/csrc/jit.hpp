@@ -42,7 +42,14 @@ bool jit_enabled();
 // pack: configurations per lane, 0 = the jit_pack policy.
 // tail: sequential-pair RNEA only -- percent of the launch's tiles run one per lane (0 none).
 // nt: the non-temporal load / store bits compiled in (RB_NT); -1 = jit_nt(kind).
-std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0, int nt = -1);
+// waves: amdgpu_waves_per_eu target of the kernel; -1 = the policy (jit_waves and the per-form
+// rules in jit_source).  jit_compile may rebuild with a 2-wave target (occupancy cliff, below).
+std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0, int nt = -1,
+                       int waves = -1);
+
+// Unified VGPR count (arch VGPRs + AGPRs) of a code object's kernel, from its AMDGPU metadata;
+// -1 if not found.
+int code_vgprs(const std::vector<char> &code);
 
 // Non-temporal access bits of `kind`'s JIT source, and the cache-key suffix of every
 // tuning value that changes the source (tuning.hpp).
@@ -61,7 +68,11 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req);
 // seq_tail; auto: 75 for the tiled layout, 0 for SoA).
 int jit_seq_tail(bool tiled);
 
-// hipRTC compilation only (no device needed): fills `code` with the code object.
+// hipRTC compilation only (no device needed): fills `code` with the code object.  Occupancy
+// cliff: a kernel built without an occupancy target that lands just past 256 registers (one
+// wave per SIMD, <= 16 over) is rebuilt with a 2-wave target -- a few spilled values cost less
+// than half the SIMD's waves (the 9-joint tree's fp64 RNEA: 258 registers; 65.0 vs 92.9 us at
+// 2^20 with 12 B of scratch).
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
                  std::vector<char> *code, std::string *error, int pack = 0, int tail = 0,
                  int nt = -1);

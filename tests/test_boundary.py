@@ -327,6 +327,34 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
         assert mb.jit_compile(f64=True, kind=kind) > 1000, kind
 
 
+def test_occupancy_cliff_rebuild(ffi, tmp_path, monkeypatch):
+    """jit_compile (jit.hpp "Occupancy cliff"): a kernel built without an occupancy target that
+    lands just past 256 registers (one wave per SIMD) is rebuilt with a 2-wave target.  The
+    9-joint tree's fp64 RNEA (258 registers) is the case; the FR3 kernels are untouched."""
+    import glob
+    import subprocess
+
+    from rigidbody_amd import chains
+
+    def vgprs(co):
+        notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True,
+                               text=True).stdout
+        return int(re.search(r"\.vgpr_count:\s+(\d+)", notes).group(1))
+
+    monkeypatch.setenv("RB_JIT_DUMP", str(tmp_path))
+    tree = ffi.Multibody.from_urdf_string(chains.tree_urdf(), ffi.URDF_TREE | ffi.GENERAL_AXES)
+    assert tree.jit_compile(True, kind="rnea") > 1000
+    co = sorted(glob.glob(str(tmp_path / "*.co")), key=os.path.getmtime)[-1]
+    assert vgprs(co) <= 256
+    assert "amdgpu_waves_per_eu(2)" in open(co[:-3] + ".hip").read()
+    assert "amdgpu_waves_per_eu" not in tree.jit_source(True, "rnea")  # the first-pass source
+    fr3 = ffi.Multibody.new()
+    for f64 in (True, False):
+        fr3.jit_compile(f64, kind="rnea")
+        co = sorted(glob.glob(str(tmp_path / "*.co")), key=os.path.getmtime)[-1]
+        assert vgprs(co) <= 128, f64
+
+
 def test_host_batch_shapes_checked(ffi):
     """The host batch wrappers check every array is [n, B] before the library copies n*B
     doubles from (and into) them: a short q would overflow the output, a short qd/tau be

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--kernel", default="rnea")
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--dof", type=int, default=7)
+    ap.add_argument("--model", choices=["chain", "tree9", "floating14"], default="chain",
+                    help="chain: FR3 (--dof 7) or the synthetic --dof chain; tree9 / floating14: the test trees")
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=5)
@@ -41,7 +43,12 @@ def main():
     a = ap.parse_args()
     dtype = bench.DT[a.dtype]
     es = 4 if a.dtype == "f32" else 8
-    mb = ffi.Multibody.new() if a.dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(a.dof))
+    if a.model != "chain":
+        floating = a.model == "floating14"
+        mb = ffi.Multibody.from_urdf_string(chains.tree_urdf(floating=floating),
+                                            ffi.FLOATING_BASE if floating else ffi.URDF_TREE | ffi.GENERAL_AXES)
+    else:
+        mb = ffi.Multibody.new() if a.dof == 7 else ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(a.dof))
     mb.upload()
     per = bench.set_bytes(mb.n, a.batch, es, a.kernel)
     nsets = max(2, int(np.ceil(1.25 * (1 << 30) / per)))
@@ -87,7 +94,8 @@ def main():
         out[v] = {"ms_median": med, "ms_min": float(np.min(ms)), "ms_rounds": [float(x) for x in ms],
                   "evals_per_s": a.batch / (med * 1e-3),
                   "hbm_frac": per / (med * 1e-3) / bench.HBM_PEAK}
-    print(json.dumps({"kernel": a.kernel, "dtype": a.dtype, "dof": a.dof, "batch": a.batch, "results": out}, indent=1))
+    print(json.dumps({"kernel": a.kernel, "dtype": a.dtype, "dof": mb.n, "model": a.model, "batch": a.batch,
+                      "results": out}, indent=1))
 
 
 if __name__ == "__main__":
