@@ -296,7 +296,7 @@ constexpr uint32_t kSplitMaxBatch = 1u << 17;
 int fd_pack(const Multibody *mb, bool f64, uint32_t B) {
     int pack = 0;
     if (rbamd::tuning().pack < 0) {
-        if (!f64 && rbamd::jit_fd_form(mb->model) == 2)
+        if (!f64 && rbamd::jit_fd_form(mb->model) == 2 && mb->model.n <= 8)  // splits measured on FR3
             pack = B <= kSplit1MaxBatch ? 5 : B <= kSplitMaxBatch ? 4 : 0;
         else  // paired lanes halve the grid: below kPackMinBatch one per lane fills more CUs
             pack = B < kPackMinBatch ? 1 : 0;
@@ -314,7 +314,8 @@ const rbamd::JitKernel *jit_fd(const Multibody *mb, bool f64, uint32_t B) {
 // 16384 43.3 vs 62.7 us (pair), 65536 43.6 vs 63.5, 131072 58.9 vs 63.7; 262144 101.5 vs 93.2
 // (profiles/r03/rollout_split/).
 int rollout_pack(const Multibody *mb, bool f64, uint32_t B) {
-    return (rbamd::tuning().pack < 0 && !f64 && B <= kSplitMaxBatch && rbamd::jit_fd_form(mb->model) == 2 &&
+    return (rbamd::tuning().pack < 0 && !f64 && B <= kSplitMaxBatch &&
+            rbamd::jit_fd_form(mb->model, rbamd::JitKind::Rollout) == 2 &&
             !(rbamd::tuning().jit_variant & 256)) ? 4 : 0;
 }
 

@@ -99,16 +99,20 @@ int jit_pack(JitKind kind, bool f64, int n) {
 
 bool jit_f64_tab(bool f64) { return f64 && tuning().f64_tab != 0; }
 
-int jit_fd_form(const Model &m) {
+int jit_fd_form(const Model &m, JitKind kind) {
     // 2 = mass-matrix forward dynamics (fdh_body.hip.hpp: RNEA bias + CRBA + L D L^T), 1 = the
     // Articulated-Body Algorithm (aba_body.hip.hpp).  The mass-matrix form holds ~n^2/2 values
     // per lane where the ABA holds ~12 per link across its sweeps, so it runs at 2-3x the
     // ABA's waves per SIMD on short chains; its O(n^2) work loses on long ones.  Trees keep
-    // the ABA (tree_body.hip.hpp).
+    // the ABA (tree_body.hip.hpp).  Forward dynamics: the mass-matrix form up to 12 links (12
+    // links 2^20 tiled: fp64 119.0 vs 159.5 us on the ABA -- 242 registers, 2 waves/SIMD, against
+    // the ABA's 398, 1 wave -- fp32 64.6 vs 75.6; 16 links: the ABA, 224 vs 229 / 101 vs 113;
+    // profiles/r05/ab/fd_form/).  Rollouts: up to 8 links (12 links x 16 steps: the ABA 2205 vs
+    // 3141 us fp64, 920 vs 959 fp32).
     if (!m.serial_revolute()) return 1;
     const int v = tuning().fd_form;
     if (v == 1 || v == 2) return v;
-    return m.n <= 8 ? 2 : 1;
+    return m.n <= (kind == JitKind::Rollout ? 8 : 12) ? 2 : 1;
 }
 
 int jit_seq_tail(bool tiled) {
@@ -122,7 +126,7 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
     // the mass-matrix forward dynamics has one- and two-per-lane forms only
     if (kind == JitKind::Fd && pack == 3 && jit_fd_form(m) == 2) return 1;
     // 4 / 5 = the bias / mass-matrix wave split, packed / one per lane: fp32 mass-matrix FD only
-    if (pack == 4 && kind == JitKind::Rollout && !(!f64 && jit_fd_form(m) == 2 && !(tuning().jit_variant & 256)))
+    if (pack == 4 && kind == JitKind::Rollout && !(!f64 && jit_fd_form(m, kind) == 2 && !(tuning().jit_variant & 256)))
         return (!f64 && m.n <= 8) ? 2 : 1;  // the split needs the mass-matrix form: the pair instead
     if ((pack == 4 || pack == 5) && kind != JitKind::Rollout && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2))
         return 1;
@@ -175,7 +179,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     if (kind == JitKind::Rollout || m.n > 8) o << "#define RB_GUARD_ANCHOR 1\n";
     // the rollout's forward dynamics follows the fd_form policy (mass-matrix form for short
     // serial chains) unless RB_VARIANT bit 8 (A/B) keeps the ABA
-    if (kind == JitKind::Rollout && jit_fd_form(m) == 2 && !(tuning().jit_variant & 256))
+    if (kind == JitKind::Rollout && jit_fd_form(m, kind) == 2 && !(tuning().jit_variant & 256))
         o << "#define RB_ROLLOUT_FDH 1\n";
     const bool tab = jit_f64_tab(f64);
     o << "#define RB_SINCOS_TAB " << (tab ? 1 : 0) << "\n";
@@ -318,7 +322,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // checks; the target keeps it there (FR3 2^20 x 16 steps, reset state: 690-708 vs 702-704 us,
     // noise-level).  Not for the ABA form: 256 VGPRs at 1 wave/SIMD runs 984 us, 2 / 3 / 4-wave
     // targets spill (1068 / 2756 / 4131 us; profiles/r05/ab/rollout_forms/).
-    if (kind == JitKind::Rollout && f64 && m.n <= 8 && jit_fd_form(m) == 2 && !(tuning().jit_variant & 256) &&
+    if (kind == JitKind::Rollout && f64 && m.n <= 8 && jit_fd_form(m, kind) == 2 && !(tuning().jit_variant & 256) &&
         tuning().jit_waves < 0 && waves_req < 0)
         waves = 4;
     if (kind == JitKind::Rnea && f64 && (tuning().jit_variant & 32768) && tuning().jit_waves < 0 && waves_req < 0)

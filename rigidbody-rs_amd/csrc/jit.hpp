@@ -61,7 +61,7 @@ int jit_pack(JitKind kind, bool f64, int n);
 std::string jit_tag(JitKind kind, bool f64, int n);
 // Forward-dynamics algorithm for this model (tuning fd_form): 2 = mass-matrix method
 // (fdh_body.hip.hpp), 1 = Articulated-Body Algorithm (aba_body.hip.hpp).
-int jit_fd_form(const Model &m);
+int jit_fd_form(const Model &m, JitKind kind = JitKind::Fd);
 // The lane form a kernel of this model really takes for the requested pack (0 = policy).
 int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req);
 // Percent of a sequential-pair RNEA launch's tiles run one per lane for this layout (tuning

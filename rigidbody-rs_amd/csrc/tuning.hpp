@@ -35,7 +35,7 @@ struct Tuning {
     // Forward dynamics algorithm of the model-specialised kernels: 1 = Articulated-Body
     // Algorithm (aba_body.hip.hpp), 2 = mass-matrix method (fdh_body.hip.hpp: bias torques by
     // RNEA, H by CRBA, L D L^T solve -- the oracle's own definition), -1 auto (jit.cpp
-    // jit_fd_form: mass matrix for serial chains up to 8 links).
+    // jit_fd_form: mass matrix for serial chains up to 12 links, rollouts up to 8).
     std::atomic<int> fd_form{-1};
     // JIT fp32 RNEA of long serial chains: the first `rnea_park` links' forces parked in LDS and
     // (cos, sin) re-evaluated from reloaded q (rnea_body.hip.hpp rnea_lane_park), 3 waves/SIMD

@@ -267,6 +267,10 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "fdh_lane" in mb.jit_source(False, "fd")             # FR3: mass-matrix FD
     assert "fdh_lane" in mb.jit_source(True, "fd")
     assert "fdh_lane" not in c30.jit_source(False, "fd")        # ... the ABA for 30 links
+    c12 = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(12))
+    for f64 in (False, True):                                   # 12 links: mass-matrix FD, one per lane
+        assert "fdh_lane<" in c12.jit_source(f64, "fd") and "fdh_lane<" in c12.jit_source(f64, "fd", batch=65536)
+        assert "RB_ROLLOUT_FDH" not in c12.jit_source(f64, "rollout")  # ... its rollouts the ABA
     assert "rnea_lane<" in mb.jit_source(False, "rnea")         # fp32 RNEA one per lane
     assert "rnea_lane_seq2<" in mb.jit_source(True, "rnea")     # fp64 RNEA: sequential pair
     assert "rnea_lane_rev<" in c30.jit_source(True, "rnea")     # ... up to 8 links; longer: reversed sweep
