@@ -11,7 +11,7 @@
  *                                 multibody_crba (multibody.rs:155-174) (SURVEY.md §8(a)
  *                                 A10), computed by exactly that definition fused per
  *                                 configuration (RNEA bias + CRBA + L D L^T) for serial chains
- *                                 up to 8 links, by the Articulated-Body Algorithm otherwise
+ *                                 up to 12 links, by the Articulated-Body Algorithm otherwise
  *                                 (rb_set_tuning "fd_form")
  *   multibody_rollout_batch_*  <- K fused forward-dynamics + semi-implicit Euler steps
  *                                 (MPC shooting)
