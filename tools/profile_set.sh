@@ -8,7 +8,7 @@
 # failing step.
 #
 # usage (via gpurun): tools/profile_set.sh NAME...
-#   NAME in: clock rnea64 rnea32 rnea32s fd64 fd32 fd32s c30 roll32 roll64
+#   NAME in: clock rnea64 rnea32 rnea32s fd64 fd32 fd32s c30 c30_64 roll32 roll64
 #            crba64 jac64 fk64 crba64t jac64t fk64t
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TRAFFIC_OUT=gpurun_out/traffic
@@ -36,6 +36,7 @@ one() {
     fd32) prof fd32 fd_fr3_f32_tiled_b1048576 --kernel fd --dtype f32 ;;
     fd32s) prof fd32s fd_fr3_f32_tiled_b65536 --kernel fd --dtype f32 --batch 65536 ;;
     c30) prof c30 rnea_chain30_f32_tiled_b1048576 --kernel rnea --dtype f32 --dof 30 ;;
+    c30_64) prof c30_64 rnea_chain30_f64_tiled_b1048576 --kernel rnea --dtype f64 --dof 30 ;;
     roll32) profany roll32 rollout_fr3_f32_K16_b1048576 tools/ab_bench.py --kernel rollout --dtype f32 \
               --variants pack=-1 --rounds 2 --steps 20 ;;
     roll64) profany roll64 rollout_fr3_f64_K16_b1048576 tools/ab_bench.py --kernel rollout --dtype f64 \
