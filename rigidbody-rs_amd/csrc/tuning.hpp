@@ -59,9 +59,12 @@ struct Tuning {
     std::atomic<int> rnea_nt{-1};
     // JIT forward dynamics / rollout: same bits as rnea_nt (-5% fp32 FD kernel time).
     std::atomic<int> fd_nt{3};
-    // JIT kernels: amdgpu_waves_per_eu occupancy target; 0 compiler's choice, -1 auto
-    // (4 for the fp32 rollout of chains up to 8 links: its K loop otherwise settles at
-    // 129+ VGPRs, one wave per SIMD fewer; 361 vs 390 us for 16 FR3 steps).
+    // JIT kernels: amdgpu_waves_per_eu occupancy target; 0 compiler's choice, -1 auto:
+    // 4 for the fp32 rollout of chains up to 8 links (its K loop otherwise settles at 129+
+    // VGPRs, one wave per SIMD fewer; 361 vs 390 us for 16 FR3 steps), for the
+    // paired fp32 mass-matrix FD and for the fp64 mass-matrix rollout (jit.cpp jit_source);
+    // 2 where a kernel built without one lands just past 256 registers (jit.cpp jit_compile,
+    // the occupancy cliff).  Any value >= 0 disables the automatic ones.
     std::atomic<int> jit_waves{-1};
     // Model constants pinned per use (spatial.hip.hpp mconst): 1 on, 0 off, -1 auto = the
     // rollout of chains up to 16 links (fp32 337 vs 1736 us; fp64 810 vs 995 us); off for
