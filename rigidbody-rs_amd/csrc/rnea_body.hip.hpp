@@ -298,11 +298,11 @@ __device__ __forceinline__ void rnea_lane_park(const T *mdl, const T *__restrict
 // orthonormal, so
 //   w_{j-1}  = E (w_j - qd z)                 aw_{j-1} = E (aw_j - qdd z - w_j x qd z)
 //   v_{j-1}  = E v_j + p x w_{j-1}            av_{j-1} = E (av_j - v_j x qd z) + p x aw_{j-1}.
-// Live set: the 12 kinematic values, the 6 of the transmitted wrench and the rows in flight,
+// Live set: the 12 kinematic values, the 6 of the transmitted wrench, qd / qdd and the rows in flight,
 // where rnea_eval holds (n, g) and (cos, sin) per link (fp64, 30 links: ~500 VGPRs, one wave per
 // SIMD; parking them in LDS as rnea_lane_park does would need 60 KB per wave).  The kinematics
-// are evaluated twice (once each way), sincos twice, and the rows are read twice (the second read
-// mostly from the Infinity Cache); the recovered kinematics carry a few extra roundings per link.
+// are evaluated twice (once each way), sincos twice, and q is read twice; the recovered
+// kinematics carry a few extra roundings per link.
 template <typename T, int N, bool FAST>
 __device__ __forceinline__ void rnea_lane_rev(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
                                               const T *__restrict__ qdd, T *__restrict__ tau, uint32_t b,
@@ -311,10 +311,10 @@ __device__ __forceinline__ void rnea_lane_rev(const T *mdl, const T *__restrict_
     constexpr int PF = 4, PB = 4;  // load distance (links) of the forward / backward sweep
     const uint32_t off = b * (uint32_t)sizeof(T);
     T qv[N], qdv[N], qddv[N];
-    auto load = [&](int j) {  // temporal: the backward sweep reads the rows again
+    auto load = [&](int j) {  // q temporal: the backward sweep reads it again
         qv[j] = ld_row<T, false>(q, j * ld, off);
-        qdv[j] = ld_row<T, false>(qd, j * ld, off);
-        qddv[j] = ld_row<T, false>(qdd, j * ld, off);
+        qdv[j] = ld_row(qd, j * ld, off);
+        qddv[j] = ld_row(qdd, j * ld, off);
     };
 #pragma unroll
     for (int j = 0; j < PF && j < N; ++j) load(j);
@@ -360,12 +360,16 @@ __device__ __forceinline__ void rnea_lane_rev(const T *mdl, const T *__restrict_
     }
     reload_fence();
     // backward sweep: rows reloaded PB links ahead, leaf first
+    // qd, qdd stay in registers from the forward sweep; only q is reloaded (30 links fp64: 184
+    // registers, 2 waves/SIMD, 227.9 vs 241.0 us tiled and 233.5 vs 258.0 SoA against reloading
+    // all three rows at 93 registers / 5 waves, whose reloads reach HBM: 1.61x the bytes)
+    auto reload = [&](int j) { qv[j] = ld_row<T, false>(q, j * ld, off); };
 #pragma unroll
-    for (int j = N - 1; j >= N - PB && j >= 0; --j) load(j);
+    for (int j = N - 1; j >= N - PB && j >= 0; --j) reload(j);
     V3<T> F, n;  // the wrench link j transmits to its parent, in link j's frame
 #pragma unroll
     for (int j = N - 1; j >= 0; --j) {
-        if (j - PB >= 0) load(j - PB);
+        if (j - PB >= 0) reload(j - PB);
         const Link<T> L = load_link(mdl, j);
         V3<T> fn, gg;
         link_force_g(L, j, st.w, st.v, st.aw, st.av, fn, gg);
