@@ -44,8 +44,9 @@ struct Tuning {
     std::atomic<int> rnea_park{-1};
     // JIT fp64 RNEA of serial chains longer than 8 links: the reversed-sweep form
     // (rnea_body.hip.hpp rnea_lane_rev: the backward sweep recovers each parent's kinematics by
-    // inverting the forward step, no per-link storage, 3-5 waves/SIMD instead of 1); 0 = off,
-    // 1 = on, -1 auto = on (12 links 2^20 tiled: 80.3 vs 107.6 us, 30 links 249 vs 328).
+    // inverting the forward step, no per-link storage, 2-3 waves/SIMD); 0 = off, 1 = on,
+    // -1 auto = on (2^20 tiled: 12 links 81.8 vs 87.2 us, 16 links 114.7 vs 112.1, 30 links 234
+    // vs 321).
     std::atomic<int> rnea_rev{-1};
 
     // ---- experimental (RB_EXPERIMENTAL=1)
