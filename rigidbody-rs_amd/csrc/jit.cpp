@@ -216,7 +216,8 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // Newton-Euler link forces about the centre of mass (spatial.hip.hpp link_force) for the
     // RNEA sweeps of chains and trees (and so the mass-matrix FD's bias): c = h / m and
     // Ic = I_o - m (|c|^2 1 - c c^T) per link (massless virtual links: c = 0, Ic = I_o = 0), in
-    // fp64 here.  jit_variant bit 9 (A/B) keeps the origin form.  Not for the fp64 RNEA: the
+    // fp64 here.  jit_variant bit 9 (A/B) keeps the origin form.  Not for the fp64 RNEA of chains
+    // up to 8 links (the reversed long-chain form below takes it): the
     // memory-bound headline kernel gains nothing from fewer VALU, its sequential pair would need
     // 131 instead of 125 VGPRs (3 waves/SIMD instead of 4), and all its grid forms (pairs,
     // single tail, one per lane below 2^19) must stay bit-identical to each other.

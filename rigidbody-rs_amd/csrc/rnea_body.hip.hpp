@@ -294,8 +294,8 @@ __device__ __forceinline__ void rnea_lane_park(const T *mdl, const T *__restrict
 // sweep (multibody.rs:122-141) carries only the link kinematics (w, v, aw, av) to the leaf; the
 // backward sweep (143-150) walks back from the leaf, each step forming link j's wrench from its
 // kinematics (link_force_g), adding the child's transmitted wrench, and recovering link j-1's
-// kinematics by inverting the forward step with the reloaded (q_j, qd_j, qdd_j) -- E_j is
-// orthonormal, so
+// kinematics by inverting the forward step with the reloaded q_j and the kept qd_j, qdd_j -- E_j
+// is orthonormal, so
 //   w_{j-1}  = E (w_j - qd z)                 aw_{j-1} = E (aw_j - qdd z - w_j x qd z)
 //   v_{j-1}  = E v_j + p x w_{j-1}            av_{j-1} = E (av_j - v_j x qd z) + p x aw_{j-1}.
 // Live set: the 12 kinematic values, the 6 of the transmitted wrench, qd / qdd and the rows in flight,
