@@ -296,7 +296,8 @@ constexpr uint32_t kSplitMaxBatch = 1u << 17;
 int fd_pack(const Multibody *mb, bool f64, uint32_t B) {
     int pack = 0;
     if (rbamd::tuning().pack < 0) {
-        if (!f64 && rbamd::jit_fd_form(mb->model) == 2 && mb->model.n <= 8)  // splits measured on FR3
+        if (!f64 && rbamd::jit_fd_form(mb->model) == 2 && mb->model.n <= 8 &&
+            mb->model.serial_revolute())  // splits: serial chains, measured on FR3
             pack = B <= kSplit1MaxBatch ? 5 : B <= kSplitMaxBatch ? 4 : 0;
         else  // paired lanes halve the grid: below kPackMinBatch one per lane fills more CUs
             pack = B < kPackMinBatch ? 1 : 0;

@@ -141,10 +141,33 @@ RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&loa
     fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) { out(j, gd.out(v)); });
 }
 
+// Kinematic trees (Topo, tree_body.hip.hpp): the same definition with the tree forms of its
+// stages -- bias torques by rnea_eval_tree at qdd = 0, H by crba_eval_tree (exact zeros for
+// joint pairs that are not ancestor / descendant), then the same L D L^T and solves.  Each stage
+// evaluates its own (cos, sin) and input checks (an out-of-domain q / qd poisons C and H, tau
+// the outputs).
+template <typename T, int N, bool FAST, typename Topo, typename Tau, typename Out>
+RB_HD void fdh_eval_tree(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&load_tau, Out &&out) {
+    T C[N], tv[N], H[N][N], Di[N], zero[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) zero[j] = T(0);
+    rnea_eval_tree<T, N, FAST, Topo>(mdl, qv, qdv, zero, [&](int j, T v) { C[j] = v; });
+    load_tau(tv);
+    reload_fence();
+    crba_eval_tree<T, N, FAST, Topo>(mdl, qv, [&](int e, T v) {
+        const int j = e % N, i = e / N;
+        if (j <= i) H[j][i] = v;
+    });
+    fdh_ldl<T, N>(H, Di);
+    InputGuard<T> gd;
+    gd.vals(tv);
+    fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) { out(j, gd.out(v)); });
+}
+
 // Lane body: loads in first-use order (q, qd root->leaf, then tau), as aba_lane.
 // Decomposition variants (jit_variant, A/B only): bit 2 = no input loads (inputs synthesised
 // from the lane index: compute + stores), bit 3 = no dynamics (loads + stores of their sum).
-template <typename T, int N, bool FAST>
+template <typename T, int N, bool FAST, typename Topo = SerialTopo>
 __device__ __forceinline__ void fdh_lane(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
                                          const T *__restrict__ tau, T *__restrict__ qdd, uint32_t b, int64_t ld) {
     const uint32_t off = b * (uint32_t)sizeof(T);
@@ -182,7 +205,10 @@ __device__ __forceinline__ void fdh_lane(const T *mdl, const T *__restrict__ q, 
 #pragma unroll
         for (int j = 0; j < N; ++j) st_row(qdd, j * ld, off, qv[j] + qdv[j] + tv[j]);
     } else {
-        fdh_eval<T, N, FAST>(mdl, qv, qdv, load_tau, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
+        if constexpr (Topo::kSerial)
+            fdh_eval<T, N, FAST>(mdl, qv, qdv, load_tau, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
+        else
+            fdh_eval_tree<T, N, FAST, Topo>(mdl, qv, qdv, load_tau, [&](int j, T v) { st_row(qdd, j * ld, off, v); });
     }
 }
 

@@ -109,8 +109,10 @@ int jit_fd_form(const Model &m, JitKind kind) {
     // the ABA's 398, 1 wave -- fp32 64.6 vs 75.6; 16 links: the ABA, 224 vs 229 / 101 vs 113;
     // profiles/r05/ab/fd_form/).  Rollouts: up to 8 links (12 links x 16 steps: the ABA 2205 vs
     // 3141 us fp64, 920 vs 959 fp32).
-    if (!m.serial_revolute()) return 1;
     const int v = tuning().fd_form;
+    // trees: the mass-matrix form only for forward dynamics and only on request (fdh_eval_tree;
+    // A/B), rollouts and the wave splits / pairs are serial-chain forms
+    if (!m.serial_revolute()) return (kind == JitKind::Fd && v == 2) ? 2 : 1;
     if (v == 1 || v == 2) return v;
     return m.n <= (kind == JitKind::Rollout ? 8 : 12) ? 2 : 1;
 }
@@ -123,6 +125,8 @@ int jit_seq_tail(bool tiled) {
 
 int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
     const int pack = pack_req > 0 ? pack_req : jit_pack(kind, f64, m.n);
+    // the tree form of the mass-matrix forward dynamics is one configuration per lane
+    if (kind == JitKind::Fd && !m.serial_revolute() && jit_fd_form(m) == 2) return 1;
     // the mass-matrix forward dynamics has one- and two-per-lane forms only
     if (kind == JitKind::Fd && pack == 3 && jit_fd_form(m) == 2) return 1;
     // 4 / 5 = the bias / mass-matrix wave split, packed / one per lane: fp32 mass-matrix FD only
@@ -393,7 +397,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
             o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
             o << "  if (b >= B) return;\n";
             o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
-            o << "  rbamd::dev::fdh_lane<T, N, " << F << ">(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
+            o << "  rbamd::dev::fdh_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, tau + o, qdd + o, threadIdx.x, ld);\n}\n";
         } else if (pack == 3) {
             o << seq_prologue;
             o << "  rbamd::dev::aba_lane_seq2<T, N, " << F

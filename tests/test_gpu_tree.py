@@ -104,6 +104,43 @@ def test_tree_batched_f64(case, dev):
 
 
 @pytest.mark.parametrize("case", CASES)
+def test_tree_fd_mass_matrix_form(case, dev):
+    """Forward dynamics of a tree by the mass-matrix method (fdh_body.hip.hpp fdh_eval_tree: tree
+    RNEA bias + tree CRBA + L D L^T; fd_form = 2) against the oracle as the ABA is held above --
+    fp64 residual 1e-8 and the CRBA solve 1e-7, fp32 residual 1e-3 norm-wise -- SoA and tiled
+    bit-identical, and a NaN input poisoning exactly its own column."""
+    from rigidbody_amd import ffi
+
+    mb, om = _setup(case)
+    B = 300
+    q, qd, _, tin = _inputs(mb, B, 13)
+    try:
+        ffi.set_tuning("fd_form", 2)
+        assert mb.kernel_path("fd", True) == "jit", ffi.last_error()
+        qdd = mb.fd_batch(_t(q, dev), _t(qd, dev), _t(tin, dev)).cpu().numpy()
+        tq, tqd, ttin = (ffi.to_tiled(_t(x, dev)) for x in (q, qd, tin))
+        qdd_t = ffi.from_tiled(mb.fd_batch_tiled(tq, tqd, ttin, B), B).cpu().numpy()
+        f = torch.float32
+        q32, qd32, t32 = (x.astype(np.float32).astype(np.float64) for x in (q, qd, tin))
+        qdd32 = mb.fd_batch(_t(q32, dev, f), _t(qd32, dev, f), _t(t32, dev, f)).cpu().numpy().astype(np.float64)
+        bad = _t(tin, dev).clone()
+        bad[2, 17] = float("nan")
+        qdd_bad = mb.fd_batch(_t(q, dev), _t(qd, dev), bad).cpu().numpy()
+    finally:
+        ffi.set_tuning("fd_form", -1)
+    res = om.rnea_batch(q, qd, qdd) - tin
+    assert (np.abs(res) / (1 + np.abs(tin))).max() <= 1e-8, f"{case} fd f64 residual (mass-matrix form)"
+    _close(qdd, om.fd_batch(q, qd, tin), 1e-7, f"{case} fd f64 vs CRBA solve (mass-matrix form)")
+    assert np.array_equal(qdd_t, qdd)
+    res32 = om.rnea_batch(q32, qd32, qdd32) - t32
+    assert (np.abs(res32).max(axis=0) / (1 + np.abs(t32).max(axis=0))).max() <= 1e-3, f"{case} fd f32 residual"
+    assert np.isnan(qdd_bad[:, 17]).all()
+    keep = np.ones(B, bool)
+    keep[17] = False
+    assert np.array_equal(qdd_bad[:, keep], qdd[:, keep])
+
+
+@pytest.mark.parametrize("case", CASES)
 def test_tree_batched_f32_and_rollout(case, dev):
     mb, om = _setup(case)
     B = 256
