@@ -857,6 +857,115 @@ def workload_name(kernel, n, dt_name, layout, B):
     return f"{kernel}_{'fr3' if n == 7 else f'chain{n}'}_{dt_name}_{layout}_b{B}"
 
 
+# ------------------------------------------------------------------ the printed line
+LINE_MAX_BYTES = 16384  # the one stdout line stays well under this (tests/test_bench_launch.py)
+
+
+def finite(x):
+    """x with every non-finite float replaced by None (strict JSON has no NaN / Infinity)."""
+    if isinstance(x, float):
+        return x if np.isfinite(x) else None
+    if isinstance(x, dict):
+        return {k: finite(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [finite(v) for v in x]
+    return x
+
+
+def _sig(x, digits=4):
+    if isinstance(x, (int, float)) and not isinstance(x, bool) and np.isfinite(x) and x != 0:
+        return float(f"{x:.{digits}g}")
+    return x
+
+
+def _summary(v):
+    """One secondary entry of the full line -> {us, frac} (+ a rate where there is no kernel time)."""
+    if not isinstance(v, dict):
+        return None
+    if "soa_us_median" in v:  # layout A/B
+        return {"soa_us": _sig(v["soa_us_median"]), "tiled_us": _sig(v["tiled_us_median"])}
+    out = {}
+    ms = v.get("kernel_ms_avg", v.get("step_ms_device", v.get("ms_per_step")))
+    if isinstance(ms, (int, float)):
+        out["us"] = _sig(ms * 1e3)
+    if isinstance(v.get("graph_ms_per_step_max_rank"), (int, float)):
+        out["graph_us"] = _sig(v["graph_ms_per_step_max_rank"] * 1e3)
+    fr = v.get("hbm_frac", v.get("hbm_frac_effective", v.get("hbm_frac_max_rank")))
+    if isinstance(fr, (int, float)):
+        out["frac"] = _sig(fr, 3)
+    iv = (v.get("valu") or {}).get("issue_frac_held")
+    if isinstance(iv, (int, float)):
+        out["valu_frac"] = _sig(iv, 3)
+    for k in ("evals_per_s", "pairs_per_s"):
+        if k in v and "us" not in out:
+            out[k] = _sig(v[k])
+    return out or None
+
+
+def compact_line(full):
+    """The ONE line bench.py prints: the contract keys, roofline, cpu_baseline and a per-workload
+    {us, frac} summary of every secondary measurement; everything else stays in the detail file
+    (write_detail).  Strict JSON, < LINE_MAX_BYTES even at --gpus 8."""
+    cfg = full["config"]
+    rf = full["roofline"]
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    line["config"] = {k: cfg[k] for k in ("workload", "kernel", "model", "split", "batch_per_gpu", "global_batch",
+                                          "parallelism", "kernel_path", "input_sets") if k in cfg}
+    line["config"]["layout"] = "tiled [B/256][n][256]" if cfg["layout"].startswith("tiled") else "SoA [n][B]"
+    line["roofline"] = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                               "bytes_per_eval", "evals_per_launch", "kernel_ms_avg")}
+    vl = rf.get("valu") or {}
+    if "issue_frac_held" in vl:
+        line["roofline"]["valu_issue_frac_held"] = vl["issue_frac_held"]
+    line["roofline"]["check"] = full.get("roofline_check", "ok")
+    if "cpu_baseline" in full:
+        cb = full["cpu_baseline"]
+        line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind") if k in cb}
+        line["cpu_baseline"]["sample"] = str(cb.get("sample", ""))[:240]
+        if "single_thread_evals_per_s" in cb:
+            line["cpu_baseline"]["single_thread_evals_per_s"] = cb["single_thread_evals_per_s"]
+    elif "cpu_baseline_note" in full:
+        line["cpu_baseline_note"] = full["cpu_baseline_note"][:200]
+    if "per_rank" in full:  # [wall s, device ms per launch] by rank
+        line["per_rank"] = [[_sig(r["wall_s"]), _sig(r["kernel_ms_avg"])] for r in full["per_rank"]]
+    sec = {}
+    for name, v in (full.get("secondary") or {}).items():
+        if name == "single_call":
+            s = {f"{k}_{w}_us": v[w][k]["median_us"] for w in ("host", "gpu") if isinstance(v.get(w), dict)
+                 for k in ("rnea", "crba") if isinstance(v[w].get(k), dict)}
+        elif name == "native_batch":
+            s = {k: _sig(x["graph_us_per_call"]) for k, x in v.items()
+                 if isinstance(x, dict) and "graph_us_per_call" in x}
+        else:
+            s = _summary(v)
+        if s:
+            sec[name] = s
+    if sec:
+        line["secondary"] = sec
+    if full.get("detail_file"):
+        line["detail_file"] = full["detail_file"]
+    return finite(line)
+
+
+def dumps_strict(obj):
+    return json.dumps(finite(obj), allow_nan=False, separators=(",", ":"))
+
+
+def write_detail(full, world):
+    """The full line (every secondary block, notes, VALU counters) to a file beside the run:
+    $RB_BENCH_DETAIL, else gpurun_out/bench_detail_n<world>.json.  Returns the path or None."""
+    path = os.environ.get("RB_BENCH_DETAIL") or os.path.join(REPO, "gpurun_out", f"bench_detail_n{world}.json")
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            f.write(json.dumps(finite(full), allow_nan=False, indent=1) + "\n")
+        return os.path.relpath(path, REPO) if path.startswith(REPO) else path
+    except OSError as e:
+        print(f"bench.py: detail file not written ({e})", file=sys.stderr)
+        return None
+
+
 def main(a):
     world, rank, dev = init_dist(a)
     n = a.dof
@@ -1008,7 +1117,13 @@ def main(a):
     viol = roofline_violations(line)
     line["roofline_check"] = "ok" if not viol else viol  # fractions <= 1, rates <= peak
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        line["detail_file"] = write_detail(line, world)
+        # the detail first (stderr: one short pointer), the compact strict-JSON line last on stdout
+        print(f"bench.py: full detail in {line['detail_file']}", file=sys.stderr, flush=True)
+        out = dumps_strict(compact_line(line))
+        if len(out) >= LINE_MAX_BYTES:
+            print(f"bench.py: compact line is {len(out)} B (>= {LINE_MAX_BYTES})", file=sys.stderr)
+        print(out, flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
 

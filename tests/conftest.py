@@ -28,6 +28,34 @@ def load_json(name):
         return json.load(f)
 
 
+def _strict_constant(c):
+    raise ValueError(f"non-strict JSON constant {c}")
+
+
+def run_bench(args, env=None, timeout=300):
+    """`python bench.py <args>` as the driver runs it: returns (the one stdout line, strict-parsed;
+    the full detail file bench.py writes beside it).  Asserts exactly one stdout line, strict JSON
+    (no NaN / Infinity tokens) and under 16 KB."""
+    import subprocess
+    import tempfile
+
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    e["RB_BENCH_DETAIL"] = os.path.join(tempfile.mkdtemp(), "detail.json")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    assert len(lines[0]) < 16384, len(lines[0])
+    line = json.loads(lines[0], parse_constant=_strict_constant)
+    with open(e["RB_BENCH_DETAIL"]) as f:
+        full = json.load(f, parse_constant=_strict_constant)
+    return line, full
+
+
 @pytest.fixture(scope="session")
 def fr3_text():
     from rigidbody_amd import chains

@@ -10,25 +10,31 @@ import sys
 
 import pytest
 
-from conftest import REPO
+from conftest import REPO, run_bench
+
+
+def _strict(_c):
+    raise ValueError(f"non-strict JSON constant {_c}")
 
 
 def _run(*args, env=None):
-    e = dict(os.environ)
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
-        e.pop(k, None)
-    e.update(env or {})
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--stub", "--steps", "5", "--warmup", "0",
-                        *args], capture_output=True, text=True, timeout=300, env=e)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
-    assert len(lines) == 1, r.stdout
-    return json.loads(lines[0])
+    """bench.py --stub: (compact stdout line, full detail file) -- conftest.run_bench."""
+    return run_bench(["--stub", "--steps", "5", "--warmup", "0", *args], env)
+
+
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline")
 
 
 @pytest.mark.parametrize("split", ["weak", "strong"])
 def test_gpus2_spawns_two_ranks(split):
-    line = _run("--gpus", "2", "--split", split)
+    compact, line = _run("--gpus", "2", "--split", split)
+    for k in REQUIRED:
+        assert k in compact, k
+    assert compact["n_gpus"] == 2 and compact["value"] == line["value"]
+    assert len(compact["per_rank"]) == 2 and compact["roofline"]["check"] == "ok"
+    if split == "weak":
+        assert set(compact["secondary"]) >= {"strong_split", "strong_split_rnea_fd"}
     assert line["n_gpus"] == 2
     assert line["scaling"] == split
     cfg = line["config"]
@@ -59,9 +65,38 @@ def test_gpus2_spawns_two_ranks(split):
 
 
 def test_single_rank_default():
-    line = _run()
+    compact, line = _run()
+    for k in REQUIRED:
+        assert k in compact, k
     assert line["n_gpus"] == 1 and line["scaling"] == "weak"
-    assert line["config"]["workload"] == "rnea_fr3_f64_tiled_b1048576"
+    assert compact["config"]["workload"] == line["config"]["workload"] == "rnea_fr3_f64_tiled_b1048576"
+    assert compact["roofline"]["bound"] == "hbm" and compact["roofline"]["unit"] == "GB/s"
+
+
+def test_compact_line_of_a_full_driver_line():
+    """The round-5 driver-style full line (22 KB, the size BENCH_r05 could not parse) through
+    bench.compact_line: strict JSON, < 16 KB, every contract key, the headline numbers unchanged,
+    a {us, frac} summary per secondary workload; and the same line grown to 8 ranks stays < 16 KB."""
+    sys.argv = ["bench.py"]
+    bench = pytest.importorskip("bench")
+    with open(os.path.join(REPO, "profiles", "r05", "session2", "bench_driver_e.json")) as f:
+        full = json.load(f)
+    assert len(json.dumps(full)) > 16384
+    full["per_rank"] = [{"rank": r, "wall_s": 1e-3, "kernel_ms_avg": 0.04, "steps": 20} for r in range(8)]
+    full["secondary"]["bad"] = {"kernel_ms_avg": float("nan"), "hbm_frac": float("inf")}
+    out = bench.dumps_strict(bench.compact_line(full))
+    assert len(out) < bench.LINE_MAX_BYTES, len(out)
+    c = json.loads(out, parse_constant=_strict)
+    for k in REQUIRED + ("cpu_baseline",):
+        assert k in c, k
+    assert c["value"] == full["value"] and c["roofline"]["frac"] == full["roofline"]["frac"]
+    assert c["cpu_baseline"]["cores"] == full["cpu_baseline"]["cores"] and c["cpu_baseline"]["kind"] == "port"
+    sec = c["secondary"]
+    assert sec["rnea_fr3_f32_b65536_graph"]["us"] > 0 and 0 < sec["fd_fr3_f64"]["frac"] <= 1
+    assert sec["layout_ab_rnea_f64"]["tiled_us"] > 0 and sec["native_batch"]
+    assert sec["bad"] == {} or all(v is None for v in sec["bad"].values())
+    for tok in ("NaN", "Infinity"):
+        assert tok not in out
 
 
 def test_failed_rank_fails_the_job():

@@ -18,7 +18,7 @@ import textwrap
 
 import pytest
 
-from conftest import PKG, REPO
+from conftest import PKG, REPO, run_bench
 
 pytestmark = pytest.mark.gpu
 
@@ -118,14 +118,10 @@ def test_bench_two_ranks_strong_rnea_fd():
     e = dict(os.environ, RB_DIST_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         e.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--split", "strong",
-                        "--kernel", "rnea_fd", "--batch", str(1 << 18), "--steps", "20", "--warmup", "5",
-                        "--no-secondary", "--no-cpu-baseline", "--spinup-ms", "50", "--rotate-gib", "0.5"],
-                       capture_output=True, text=True, timeout=300, env=e)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    line = json.loads(lines[0])
+    compact, line = run_bench(["--gpus", "2", "--split", "strong", "--kernel", "rnea_fd", "--batch", str(1 << 18),
+                               "--steps", "20", "--warmup", "5", "--no-secondary", "--no-cpu-baseline",
+                               "--spinup-ms", "50", "--rotate-gib", "0.5"], e)
+    assert compact["value"] == line["value"] and len(compact["per_rank"]) == 2
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["global_batch"] == 1 << 18 and line["config"]["batch_per_gpu"] == 1 << 17
     assert line["value"] > 0 and line["config"]["kernel_path"] == "jit+jit"
@@ -141,13 +137,9 @@ def test_bench_two_ranks_weak_with_strong_split():
     e = dict(os.environ, RB_DIST_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         e.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--batch", str(1 << 18),
-                        "--steps", "20", "--warmup", "5", "--no-secondary", "--no-cpu-baseline", "--spinup-ms", "50",
-                        "--rotate-gib", "0.5"], capture_output=True, text=True, timeout=300, env=e)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    line = json.loads(lines[0])
+    compact, line = run_bench(["--gpus", "2", "--batch", str(1 << 18), "--steps", "20", "--warmup", "5",
+                               "--no-secondary", "--no-cpu-baseline", "--spinup-ms", "50", "--rotate-gib", "0.5"], e)
+    assert set(compact["secondary"]) >= {"strong_split", "strong_split_rnea_fd"}
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["steps"] == 20
     assert len(line["per_rank"]) == 2 and all(x["steps"] == 20 for x in line["per_rank"])
     st = line["secondary"]["strong_split"]
