@@ -54,8 +54,9 @@ def parse(argv=None):
                     help="f64 = the reference's Real (lib.rs:15), the headline; f32 is a reduced-precision "
                          "variant reported under 'secondary'")
     ap.add_argument("--kernel", choices=["rnea", "fd", "rnea_fd"], default="rnea",
-                    help="rnea_fd = SURVEY §8(d) config 4: each step runs RNEA then forward dynamics on "
-                         "its torques (q, qd, qdd -> tau -> qdd'), 8·N·s bytes per configuration")
+                    help="rnea_fd = SURVEY §8(d) config 4: each step evaluates tau = rnea(q, qd, qdd) and "
+                         "qdd' = fd(q, qd, tau_in) (multibody_rnea_fd_batch_*, one fused launch), 6·n·s bytes "
+                         "per configuration")
     ap.add_argument("--dof", type=int, default=7, help="7 = FR3; other values = synthetic z-chain")
     ap.add_argument("--layout", choices=["tiled", "soa"], default="tiled",
                     help="device array layout: tiled [B/256][n][256] (rigidbody_batch.h *_tiled entry points, "
@@ -187,8 +188,8 @@ def load_model(world, rank, dof, dev):
 
 
 def make_sets(mb, B, dtype, kernel, nsets, seed, layout="soa"):
-    """nsets independent (inputs, outputs) sets on the device.  rnea / rnea_fd read
-    (q, qd, qdd); fd reads (q, qd, tau).  rnea_fd has two outputs (tau, qdd').
+    """nsets independent (inputs, outputs) sets on the device.  rnea reads (q, qd, qdd); fd
+    reads (q, qd, tau); rnea_fd reads (q, qd, qdd, tau_in) and has two outputs (tau, qdd').
     layout "tiled": [ceil(B/256), n, 256] tensors (rigidbody_batch.h), filled with the
     same values as the SoA sets (device fill, then rb_to_tiled)."""
     if layout == "tiled":
@@ -199,7 +200,7 @@ def make_sets(mb, B, dtype, kernel, nsets, seed, layout="soa"):
         torch.cuda.synchronize()
         return sets
     lim = mb.limits()
-    kinds = ("q", "qd", "tau") if kernel == "fd" else ("q", "qd", "qdd")
+    kinds = {"fd": ("q", "qd", "tau"), "rnea_fd": ("q", "qd", "qdd", "tau")}.get(kernel, ("q", "qd", "qdd"))
     nout = 2 if kernel == "rnea_fd" else 1
     sets = []
     for s in range(nsets):
@@ -216,9 +217,9 @@ def make_sets(mb, B, dtype, kernel, nsets, seed, layout="soa"):
 
 
 def set_bytes(n, B, esize, kernel):
-    """Algorithmic HBM bytes: q, qd, qdd|tau read + tau|qdd written, 4·N·s per
-    configuration; rnea_fd counts both kernels."""
-    return (8 if kernel == "rnea_fd" else 4) * n * B * esize
+    """Algorithmic HBM bytes: q, qd, qdd|tau read + tau|qdd written, 4·n·s per
+    configuration; rnea_fd reads q, qd, qdd, tau_in and writes tau, qdd', 6·n·s."""
+    return (6 if kernel == "rnea_fd" else 4) * n * B * esize
 
 
 def nsets_for(n, B, esize, kernel, rotate_gib):
@@ -318,21 +319,20 @@ def batch_launcher(mb, sets, kernel, dtype, layout="soa", B=None):
     lib = ffi.lib()
     suffix = "f32" if dtype == torch.float32 else "f64"
     ns = len(sets)
+    lay = "tiled_" if layout == "tiled" else ""
+    rnea = getattr(lib, f"multibody_rnea_batch_{lay}{suffix}")
+    fd = getattr(lib, f"multibody_fd_batch_{lay}{suffix}")
+    idfd = getattr(lib, f"multibody_rnea_fd_batch_{lay}{suffix}")
     if layout == "tiled":
-        rnea = getattr(lib, f"multibody_rnea_batch_tiled_{suffix}")
-        fd = getattr(lib, f"multibody_fd_batch_tiled_{suffix}")
         tail = (B,)
     else:
-        rnea = getattr(lib, f"multibody_rnea_batch_{suffix}")
-        fd = getattr(lib, f"multibody_fd_batch_{suffix}")
         B = sets[0][1][0].shape[1]
         tail = (B, B)
     calls = []
     for i, o in sets:
         p = [t.data_ptr() for t in i] + [t.data_ptr() for t in o]
         if kernel == "rnea_fd":
-            calls.append(((rnea, (mb.handle, p[0], p[1], p[2], p[3]) + tail),
-                          (fd, (mb.handle, p[0], p[1], p[3], p[4]) + tail)))
+            calls.append(((idfd, (mb.handle,) + tuple(p) + tail),))
         else:
             calls.append(((rnea if kernel == "rnea" else fd, (mb.handle, p[0], p[1], p[2], p[3]) + tail),))
 
@@ -505,10 +505,8 @@ def side_workloads(mb7, a):
         sec[name] = {"evals_per_s": B * r["steps"] / r["wall"], "kernel_ms_avg": r["kernel_ms_avg"], "batch": B,
                      "launches": r["steps"],
                      "layout": layout, "dtype": dt_name, "hbm_frac": r["bytes"] / (r["kernel_ms_avg"] * 1e-3) / HBM_PEAK,
-                     "kernel_path": "+".join(mb.kernel_path(k, dt_name == "f64", B, layout == "tiled")
-                                             for k in kernel.split("_")),
-                     "kernel_form": "+".join(str(mb.kernel_form(k, dt_name == "f64", B, layout == "tiled"))
-                                             for k in kernel.split("_"))}
+                     "kernel_path": mb.kernel_path(kernel, dt_name == "f64", B, layout == "tiled"),
+                     "kernel_form": str(mb.kernel_form(kernel, dt_name == "f64", B, layout == "tiled"))}
         if kernel in ("rnea", "fd"):
             model = "fr3" if mb.n == 7 else f"chain{mb.n}" if "tree" not in name else None
             if model:
@@ -626,7 +624,8 @@ def single_call(iters=2000):
     return out
 
 
-def native_batch(cases=(("rnea", "f32", 65536), ("fd", "f32", 65536), ("rnea", "f64", 131072), ("fd", "f64", 131072))):
+def native_batch(cases=(("rnea", "f32", 65536), ("fd", "f32", 65536), ("rnea", "f64", 131072), ("fd", "f64", 131072),
+                        ("rnea_fd", "f64", 131072), ("rnea+fd", "f64", 131072))):
     """SURVEY §8(d) configs 2 / 3 (and config 4's 2^17 fp64 shard) as a native caller drives the
     batched C ABI: examples/batch_bench.cpp, a child process linked against
     librigidbody_bindings.so -- eager back-to-back calls on one stream (and their host cost per
@@ -639,9 +638,10 @@ def native_batch(cases=(("rnea", "f32", 65536), ("fd", "f32", 65536), ("rnea", "
         r = subprocess.run([exe, kind, dt, str(B), "20000", "tiled"], capture_output=True, text=True, timeout=300)
         key = f"{kind}_fr3_{dt}_b{B}"
         out[key] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {"error": r.stderr[-500:]}
-    out["how"] = ("C++ consumer (examples/batch_bench.cpp): 20000 calls of multibody_{rnea,fd}_batch_tiled_* over "
-                  "input sets rotated through >= 1.25 GiB, hipEvent pair on the stream; eager = back-to-back calls, "
-                  "graph = the same calls captured 100 per HIP graph and replayed")
+    out["how"] = ("C++ consumer (examples/batch_bench.cpp): 20000 calls of multibody_{rnea,fd,rnea_fd}_batch_tiled_* "
+                  "over input sets rotated through >= 1.25 GiB, hipEvent pair on the stream; eager = back-to-back "
+                  "calls, graph = the same calls captured 100 per HIP graph and replayed; rnea+fd = config 4's pair "
+                  "as two calls (rnea then fd), rnea_fd = the same pair in one fused call")
     return out
 
 
@@ -691,15 +691,15 @@ def cpu_baseline(n, kernel, cpu_seconds):
     cores, how = cpu_share()
     mbl = ([l["lower"] for l in raw["limits"]], [l["upper"] for l in raw["limits"]],
            [l["velocity"] for l in raw["limits"]], [l["effort"] for l in raw["limits"]])
-    kinds = ("q", "qd", "tau") if kernel == "fd" else ("q", "qd", "qdd")
+    kinds = {"fd": ("q", "qd", "tau"), "rnea_fd": ("q", "qd", "qdd", "tau")}.get(kernel, ("q", "qd", "qdd"))
 
     def inputs(B):
         return [chains.host_uniform(n, B, *chains.input_ranges(mbl, kind), chains.SEED + k)
                 for k, kind in enumerate(kinds)]
 
     if kernel == "rnea_fd":
-        def call(q, qd, qdd, nthreads):
-            return om.fd_batch(q, qd, om.rnea_batch(q, qd, qdd, nthreads=nthreads), nthreads=nthreads)
+        def call(q, qd, qdd, tau, nthreads):
+            return om.rnea_batch(q, qd, qdd, nthreads=nthreads), om.fd_batch(q, qd, tau, nthreads=nthreads)
     else:
         call = om.rnea_batch if kernel == "rnea" else om.fd_batch
     cal = inputs(20000)
@@ -990,7 +990,7 @@ def main(a):
     else:
         r = measure(mb, a.kernel, a.dtype, B, a.layout, a.steps, a.warmup, world, a.rotate_gib, seed, a.spinup_ms,
                     a.streams, a.sync_every)
-        kpath = "+".join(mb.kernel_path(k, a.dtype == "f64", B, a.layout == "tiled") for k in a.kernel.split("_"))
+        kpath = mb.kernel_path(a.kernel, a.dtype == "f64", B, a.layout == "tiled")
     ranks = per_rank(r, world, dev)
     wall, kern_ms = rdist.max_over_ranks([r["wall"], r["kernel_ms_avg"]], world, dev)
     value = global_batch * a.steps / wall
@@ -1073,7 +1073,7 @@ def main(a):
             # launches replayed from a HIP graph give the device-bound rate beside them
             r4 = measure(mb, "rnea_fd", "f64", c4hi - c4lo, a.layout, None, 5, world, a.rotate_gib, chains.SEED,
                          100.0, graph=True, dev=dev)
-            k4 = "+".join(mb.kernel_path(k, True, c4hi - c4lo, a.layout == "tiled") for k in ("rnea", "fd"))
+            k4 = mb.kernel_path("rnea_fd", True, c4hi - c4lo, a.layout == "tiled")
         w4, km4 = rdist.max_over_ranks([r4["wall"], r4["kernel_ms_avg"]], world, dev)
         g4 = rdist.max_over_ranks([r4.get("graph_kernel_ms_avg", 0.0)], world, dev)[0]
         b4 = set_bytes(n, 1, 8, "rnea_fd")

@@ -12,7 +12,10 @@
 //           own floor)
 //   graph   the same calls captured once into a HIP graph (100 per graph) and replayed
 //
-// usage: batch_bench KIND DTYPE B [K] [tiled]   KIND rnea|fd, DTYPE f32|f64
+// usage: batch_bench KIND DTYPE B [K] [tiled]   KIND rnea|fd|rnea_fd|rnea+fd, DTYPE f32|f64
+//   rnea_fd: multibody_rnea_fd_batch_* (tau = rnea(q, qd, qdd), qdd' = fd(q, qd, tau_in), one launch);
+//   rnea+fd: the same pair as two calls, multibody_rnea_batch_* then multibody_fd_batch_* (config 4
+//   before the fused entry point)
 //   -> one JSON object on stdout.
 #include <hip/hip_runtime.h>
 
@@ -45,14 +48,15 @@ namespace {
     } while (0)
 
 struct Set {
-    void *in[3];
-    void *out;
+    void *in[4];  // q, qd, qdd | tau, tau_in (rnea_fd / rnea+fd)
+    void *out[2];
 };
 
+enum Kind { kRnea, kFd, kRneaFd, kRneaThenFd };
+
 template <typename T>
-int call(const Multibody *mb, bool fd, bool tiled, const Set &s, int64_t B, hipStream_t st) {
-    const T *a = (const T *)s.in[0], *b = (const T *)s.in[1], *c = (const T *)s.in[2];
-    T *o = (T *)s.out;
+int call1(const Multibody *mb, bool fd, bool tiled, const T *a, const T *b, const T *c, T *o, int64_t B,
+          hipStream_t st) {
     if constexpr (sizeof(T) == 4) {
         if (tiled) return fd ? multibody_fd_batch_tiled_f32(mb, a, b, c, o, B, st) : multibody_rnea_batch_tiled_f32(mb, a, b, c, o, B, st);
         return fd ? multibody_fd_batch_f32(mb, a, b, c, o, B, B, st) : multibody_rnea_batch_f32(mb, a, b, c, o, B, B, st);
@@ -63,8 +67,32 @@ int call(const Multibody *mb, bool fd, bool tiled, const Set &s, int64_t B, hipS
 }
 
 template <typename T>
-int run(const char *kind, int64_t B, int K, bool tiled) {
-    const bool fd = std::strcmp(kind, "fd") == 0;
+int call(const Multibody *mb, Kind kind, bool tiled, const Set &s, int64_t B, hipStream_t st) {
+    const T *a = (const T *)s.in[0], *b = (const T *)s.in[1], *c = (const T *)s.in[2], *d = (const T *)s.in[3];
+    T *o = (T *)s.out[0], *o2 = (T *)s.out[1];
+    if (kind == kRnea || kind == kFd) return call1<T>(mb, kind == kFd, tiled, a, b, c, o, B, st);
+    if (kind == kRneaThenFd) {
+        if (int rc = call1<T>(mb, false, tiled, a, b, c, o, B, st)) return rc;
+        return call1<T>(mb, true, tiled, a, b, d, o2, B, st);
+    }
+    if constexpr (sizeof(T) == 4) {
+        return tiled ? multibody_rnea_fd_batch_tiled_f32(mb, a, b, c, d, o, o2, B, st)
+                     : multibody_rnea_fd_batch_f32(mb, a, b, c, d, o, o2, B, B, st);
+    } else {
+        return tiled ? multibody_rnea_fd_batch_tiled_f64(mb, a, b, c, d, o, o2, B, st)
+                     : multibody_rnea_fd_batch_f64(mb, a, b, c, d, o, o2, B, B, st);
+    }
+}
+
+template <typename T>
+int run(const char *kind_s, int64_t B, int K, bool tiled) {
+    const Kind kind = !std::strcmp(kind_s, "fd") ? kFd : !std::strcmp(kind_s, "rnea_fd") ? kRneaFd
+                      : !std::strcmp(kind_s, "rnea+fd") ? kRneaThenFd : kRnea;
+    const bool fd = kind == kFd;
+    const bool pair = kind == kRneaFd || kind == kRneaThenFd;
+    const int nin = pair ? 4 : 3, nout = pair ? 2 : 1;
+    // multibody_kernel_path_ex / _form_ex kind: 0 rnea, 1 fd, 6 rnea_fd
+    const int qkind = kind == kFd ? 1 : kind == kRneaFd ? 6 : 0;
     Multibody *mb = multibody_new();
     if (!mb) {
         std::fprintf(stderr, "multibody_new: %s\n", rb_last_error());
@@ -74,25 +102,27 @@ int run(const char *kind, int64_t B, int K, bool tiled) {
     std::vector<double> lo(n), hi(n), vel(n), eff(n);
     multibody_limits(mb, lo.data(), hi.data(), vel.data(), eff.data());
     // input ranges as chains.input_ranges: q in the limits, qd +-velocity, qdd +-10, tau +-effort
-    std::vector<double> rlo[3], rhi[3];
-    for (int k = 0; k < 3; ++k) rlo[k].resize(n), rhi[k].resize(n);
+    std::vector<double> rlo[4], rhi[4];
+    for (int k = 0; k < 4; ++k) rlo[k].resize(n), rhi[k].resize(n);
     for (int j = 0; j < n; ++j) {
         rlo[0][j] = std::isnan(lo[j]) ? -M_PI : lo[j];
         rhi[0][j] = std::isnan(hi[j]) ? M_PI : hi[j];
         rlo[1][j] = -vel[j], rhi[1][j] = vel[j];
         rlo[2][j] = fd ? -eff[j] : -10.0, rhi[2][j] = fd ? eff[j] : 10.0;
+        rlo[3][j] = -eff[j], rhi[3][j] = eff[j];
     }
     // tiled arrays are [ceil(B/256)][n][256] (filled as SoA rows, then rb_to_tiled); SoA [n][B]
     const int64_t cols = tiled ? ((B + 255) / 256) * 256 : B;
     const size_t bytes = (size_t)n * (size_t)cols * sizeof(T);
     void *soa = nullptr;
     CHECK_HIP(hipMalloc(&soa, (size_t)n * (size_t)B * sizeof(T)));
-    const int nsets = std::max<int>(2, (int)std::ceil(1.25 * (1 << 30) / (4.0 * (double)bytes)));
+    const int nsets = std::max<int>(2, (int)std::ceil(1.25 * (1 << 30) / ((nin + nout) * (double)bytes)));
     std::vector<Set> sets(nsets);
     hipStream_t st;
     CHECK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     for (int s = 0; s < nsets; ++s) {
-        for (int k = 0; k < 3; ++k) {
+        sets[s].in[3] = sets[s].out[1] = nullptr;
+        for (int k = 0; k < nin; ++k) {
             CHECK_HIP(hipMalloc(&sets[s].in[k], bytes));
             void *dst = tiled ? soa : sets[s].in[k];
             int rc = sizeof(T) == 4 ? rb_fill_uniform_f32((float *)dst, n, B, B, rlo[k].data(), rhi[k].data(), 1000 * s + k, st)
@@ -105,16 +135,17 @@ int run(const char *kind, int64_t B, int K, bool tiled) {
                 return 1;
             }
         }
-        CHECK_HIP(hipMalloc(&sets[s].out, bytes));
+        for (int k = 0; k < nout; ++k) CHECK_HIP(hipMalloc(&sets[s].out[k], bytes));
     }
     CHECK_HIP(hipStreamSynchronize(st));
     CHECK_HIP(hipFree(soa));
     multibody_upload(mb);
     // pre-build the kernel this launch shape takes (hipRTC at first use), as INTEGRATION.md asks
     // before graph capture
-    multibody_kernel_path_ex(mb, fd ? 1 : 0, sizeof(T) == 8, B, tiled);
+    multibody_kernel_path_ex(mb, qkind, sizeof(T) == 8, B, tiled);
+    if (kind == kRneaThenFd) multibody_kernel_path_ex(mb, 1, sizeof(T) == 8, B, tiled);
     auto launch = [&](int i) {
-        if (call<T>(mb, fd, tiled, sets[i % nsets], B, st)) {
+        if (call<T>(mb, kind, tiled, sets[i % nsets], B, st)) {
             std::fprintf(stderr, "launch: %s\n", rb_last_error());
             std::exit(1);
         }
@@ -166,14 +197,16 @@ int run(const char *kind, int64_t B, int K, bool tiled) {
                 "\"graph_us_per_call\": %.3f, "
                 "\"eager_evals_per_s\": %.4g, \"graph_evals_per_s\": %.4g, \"input_sets\": %d, "
                 "\"kernel_form\": %d}\n",
-                kind, sizeof(T) == 4 ? "f32" : "f64", (long long)B, tiled ? "tiled" : "soa", K, eager_us, host_us,
+                kind_s, sizeof(T) == 4 ? "f32" : "f64", (long long)B, tiled ? "tiled" : "soa", K, eager_us, host_us,
                 empty_host_us, graph_us, B / (eager_us * 1e-6), B / (graph_us * 1e-6), nsets,
-                multibody_kernel_form_ex(mb, fd ? 1 : 0, sizeof(T) == 8, B, tiled));
+                multibody_kernel_form_ex(mb, qkind, sizeof(T) == 8, B, tiled));
     CHECK_HIP(hipGraphExecDestroy(ge));
     CHECK_HIP(hipGraphDestroy(g));
     for (auto &s : sets) {
-        for (void *p : s.in) CHECK_HIP(hipFree(p));
-        CHECK_HIP(hipFree(s.out));
+        for (void *p : s.in)
+            if (p) CHECK_HIP(hipFree(p));
+        for (void *p : s.out)
+            if (p) CHECK_HIP(hipFree(p));
     }
     CHECK_HIP(hipStreamDestroy(st));
     multibody_free(mb);
@@ -184,7 +217,7 @@ int run(const char *kind, int64_t B, int K, bool tiled) {
 
 int main(int argc, char **argv) {
     if (argc < 4) {
-        std::fprintf(stderr, "usage: %s rnea|fd f32|f64 B [K] [tiled]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s rnea|fd|rnea_fd|rnea+fd f32|f64 B [K] [tiled]\n", argv[0]);
         return 2;
     }
     const int64_t B = std::atoll(argv[3]);

@@ -13,6 +13,9 @@
  *                                 configuration (RNEA bias + CRBA + L D L^T) for serial chains
  *                                 up to 12 links, by the Articulated-Body Algorithm otherwise
  *                                 (rb_set_tuning "fd_form")
+ *   multibody_rnea_fd_batch_*  <- both of the above on one (q, qd): tau = rnea(q, qd, qdd) and
+ *                                 qdd' = fd(q, qd, tau_in) in one launch (SURVEY.md §8(d)
+ *                                 config 4's RNEA + forward-dynamics pair)
  *   multibody_rollout_batch_*  <- K fused forward-dynamics + semi-implicit Euler steps
  *                                 (MPC shooting)
  *   multibody_crba_batch_*     <- multibody_crba      (lib.rs:32-43)
@@ -132,10 +135,11 @@ int multibody_upload(const Multibody *mb);
 
 /* Which kernel a launch of `batch` configurations (tiled != 0: the *_tiled entry points)
  * runs for this model on the current device; kind 0 = rnea, 1 = fd, 2 = crba, 3 = rollout,
- * 4 = fwd_kin, 5 = jac.  1 = model-specialised kernel compiled at first use by hipRTC (this
- * call compiles exactly the form such a launch takes), 0 = precompiled generic kernel (also
- * when hipRTC failed; rb_last_error() holds the log -- a tree model's calls then fail with
- * RB_ERR_UNSUPPORTED).  multibody_kernel_path = a 2^20-configuration SoA launch. */
+ * 4 = fwd_kin, 5 = jac, 6 = rnea_fd (multibody_rnea_fd_batch_*).  1 = model-specialised kernel
+ * compiled at first use by hipRTC (this call compiles exactly the form such a launch takes), 0 =
+ * precompiled generic kernel (also when hipRTC failed; rb_last_error() holds the log -- a tree
+ * model's calls then fail with RB_ERR_UNSUPPORTED; kind 6: the model has no fused kernel and
+ * runs the rnea then the fd kernel).  multibody_kernel_path = a 2^20-configuration SoA launch. */
 int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled);
 int multibody_kernel_path(const Multibody *mb, int kind, int f64);
 int multibody_rnea_kernel_path(const Multibody *mb, int f64);
@@ -199,6 +203,30 @@ int multibody_fd_batch_tiled_f32(const Multibody *mb, const float *q, const floa
                                  float *qdd, int64_t batch, void *stream);
 int multibody_fd_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
                                  double *qdd, int64_t batch, void *stream);
+/* Inverse and forward dynamics of the same (q, qd) in one launch:
+ *   tau     = rnea(q, qd, qdd)                   (multibody_rnea_batch_*, multibody.rs:111-153)
+ *   qdd_out = sym(H)^-1 (tau_in - rnea(q, qd, 0)) (multibody_fd_batch_*)
+ * For models on the mass-matrix forward dynamics (serial revolute chains up to 12 links) one
+ * fused kernel evaluates both from one set of factors: the bias torques C = rnea(q, qd, 0), H
+ * (multibody.rs:155-174) and its L D L^T, with tau = C + sym(H) qdd -- the RNEA is affine in qdd
+ * with slope H -- so q and qd are read once: 6 n s bytes per configuration against 8 n s for
+ * the two calls, and one launch.  tau agrees with multibody_rnea_batch_* to rounding (not bit
+ * for bit: a different order of the same sums; tested against the oracle at 1e-9 scaled in
+ * fp64), qdd_out with multibody_fd_batch_* bit for bit.  Other models run the two kernels
+ * back to back on `stream`.  Input domain as above, per output: tau is NaN for a configuration
+ * whose q, qd or qdd is out of the domain, qdd_out for one whose q, qd or tau_in is.  Outputs
+ * must not overlap the inputs. */
+int multibody_rnea_fd_batch_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                const float *tau_in, float *tau, float *qdd_out, int64_t batch, int64_t ld,
+                                void *stream);
+int multibody_rnea_fd_batch_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                const double *tau_in, double *tau, double *qdd_out, int64_t batch, int64_t ld,
+                                void *stream);
+int multibody_rnea_fd_batch_tiled_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                      const float *tau_in, float *tau, float *qdd_out, int64_t batch, void *stream);
+int multibody_rnea_fd_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                      const double *tau_in, double *tau, double *qdd_out, int64_t batch,
+                                      void *stream);
 /* SoA [rows][ld] <-> tiled [ceil(batch/256)][rows][256] (to_tiled zero-fills the tail lanes). */
 int rb_to_tiled_f32(const float *src, int64_t ld, float *dst, int rows, int64_t batch, void *stream);
 int rb_to_tiled_f64(const double *src, int64_t ld, double *dst, int rows, int64_t batch, void *stream);

@@ -34,7 +34,7 @@
 
 #define RB_VERSION "rigidbody-rs_amd 0.2.0 (gfx950)"
 
-static const char *const kKindMsg = "kind must be 0 rnea, 1 fd, 2 crba, 3 rollout, 4 fwd_kin or 5 jac";
+static const char *const kKindMsg = "kind must be 0 rnea, 1 fd, 2 crba, 3 rollout, 4 fwd_kin, 5 jac or 6 rnea_fd";
 
 namespace {
 
@@ -97,7 +97,7 @@ struct Multibody {
         const rbamd::JitKernel *jk = nullptr;
     };
     mutable std::map<std::pair<const void *, const rbamd::JitKernel *>, JitPub> jit_pub;
-    mutable std::atomic<const JitPub *> jit_fast[16][6][2][2][6][4] = {};  // last: tail > 0, nt override
+    mutable std::atomic<const JitPub *> jit_fast[16][rbamd::kJitKinds][2][2][6][4] = {};  // last: tail > 0, nt override
     // device_consts fast path: the uploaded constant blocks per device (set once, never moved)
     mutable std::atomic<const void *> dc_fast[16][2] = {};
 };
@@ -184,7 +184,7 @@ const rbamd::JitKernel *jit_get(const Multibody *mb, rbamd::JitKind kind, bool f
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
     const bool fst = fast && !f64;
     std::atomic<const Multibody::JitPub *> *slot = nullptr;
-    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < 6 && pack >= 0 && pack < 6) {
+    if (d >= 0 && d < 16 && (int)kind >= 0 && (int)kind < rbamd::kJitKinds && pack >= 0 && pack < 6) {
         slot = &mb->jit_fast[d][(int)kind][f64 ? 1 : 0][fst ? 1 : 0][pack][(tail > 0 ? 1 : 0) | (nt >= 0 ? 2 : 0)];
         if (const Multibody::JitPub *p = slot->load(std::memory_order_acquire))
             if (p->gen.load(std::memory_order_acquire) == rbamd::tuning_generation()) return p->jk;
@@ -384,6 +384,30 @@ hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T 
     return rbamd::launch_aba<T>(mb->model.n, mdl, q, qd, tau, qdd, B, ld, s, fast_trig(), tiled);
 }
 
+// Inverse + forward dynamics of the same (q, qd) (config 4's pair): one fused hipRTC launch
+// (fdh_body.hip.hpp idfd_lane) for models on the mass-matrix forward dynamics; otherwise -- the
+// ABA models (trees, chains over 12 links), hipRTC off or failed -- the RNEA launch then the
+// forward-dynamics launch, the same results.
+const rbamd::JitKernel *jit_idfd(const Multibody *mb, bool f64) {
+    if (!mb->model.serial_revolute() || rbamd::jit_fd_form(mb->model, rbamd::JitKind::RneaFd) != 2) return nullptr;
+    return jit_get(mb, rbamd::JitKind::RneaFd, f64, !f64 && fast_trig());
+}
+
+template <typename T>
+hipError_t launch_idfd_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *qdd, const T *tau_in,
+                           T *tau, T *qdd_out, uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
+    if (B == 0) return hipSuccess;
+    if (const rbamd::JitKernel *jk = jit_idfd(mb, sizeof(T) == 8)) {
+        const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
+        void *args[] = {(void *)&q,   (void *)&qd, (void *)&qdd,  (void *)&tau_in, (void *)&tau,
+                        (void *)&qdd_out, (void *)&B, (void *)&lda, (void *)&bs};
+        return jit_launch(jk, B, args, s);
+    }
+    hipError_t e = launch_rnea_any<T>(mb, mdl, q, qd, qdd, tau, B, ld, s, tiled);
+    if (e != hipSuccess) return e;
+    return launch_fd_any<T>(mb, mdl, q, qd, tau_in, qdd_out, B, ld, s, tiled);
+}
+
 template <typename T>
 hipError_t launch_rollout_any(const Multibody *mb, const T *mdl, T *q, T *qd, const T *tau_seq, T dt, int K, T *traj,
                               uint32_t B, int64_t ld, hipStream_t s) {
@@ -574,6 +598,24 @@ int fd_batch(const Multibody *mb, const T *q, const T *qd, const T *tau, T *qdd,
         const int64_t o = b0 * per;
         hipError_t e = launch_fd_any<T>(mb, mdl, q + o, qd + o, tau + o, qdd + o, nb, ld, (hipStream_t)stream, tiled);
         return e == hipSuccess ? RB_OK : hip_err(e, "aba launch");
+    });
+}
+
+template <typename T>
+int idfd_batch(const Multibody *mb, const T *q, const T *qd, const T *qdd, const T *tau_in, T *tau, T *qdd_out,
+               int64_t batch, int64_t ld, void *stream, bool tiled = false) {
+    int rc = check_batch(mb, batch, tiled ? batch : ld);
+    if (rc) return rc;
+    if (batch == 0) return RB_OK;
+    if (!q || !qd || !qdd || !tau_in || !tau || !qdd_out) return set_err(RB_ERR_NULL, "NULL array");
+    const T *mdl = nullptr;
+    if ((rc = device_consts<T>(mb, &mdl))) return rc;
+    const int64_t per = tiled ? mb->model.n : 1;
+    return chunked<T>(batch, [&](int64_t b0, uint32_t nb) {
+        const int64_t o = b0 * per;
+        hipError_t e = launch_idfd_any<T>(mb, mdl, q + o, qd + o, qdd + o, tau_in + o, tau + o, qdd_out + o, nb, ld,
+                                          (hipStream_t)stream, tiled);
+        return e == hipSuccess ? RB_OK : hip_err(e, "rnea_fd launch");
     });
 }
 
@@ -899,19 +941,20 @@ namespace {
 // launchers (launch_*_any).  *generic = true when the precompiled kernel runs (serial revolute
 // fwd_kin / jac, JIT disabled or failed).
 const rbamd::JitKernel *resolve_kernel(const Multibody *mb, int kind, bool f64, int64_t batch, bool tiled) {
-    if (kind >= 4 && kin_precompiled(mb)) return nullptr;  // precompiled kinematics
+    if ((kind == 4 || kind == 5) && kin_precompiled(mb)) return nullptr;  // precompiled kinematics
     if (!rbamd::jit_enabled()) return nullptr;
     const uint32_t B = batch < kChunk ? (uint32_t)batch : (uint32_t)kChunk;
     if (kind == 0) return jit_rnea(mb, f64, B, tiled);
     if (kind == 1) return jit_fd(mb, f64, B);
     if (kind == 3) return jit_rollout(mb, f64, B);
+    if (kind == 6) return jit_idfd(mb, f64);
     if (kind >= 4) return jit_kin(mb, kind == 5, f64);
     return jit_get(mb, rbamd::JitKind::Crba, f64, false);
 }
 
 int check_kernel_query(const Multibody *mb, int kind, int64_t batch) {
     if (!mb) return set_err(RB_ERR_NULL, "NULL Multibody handle");
-    if (kind < 0 || kind > 5) return set_err(RB_ERR_ARG, kKindMsg);
+    if (kind < 0 || kind >= rbamd::kJitKinds) return set_err(RB_ERR_ARG, kKindMsg);
     if (batch < 1) return set_err(RB_ERR_ARG, "batch must be positive");
     return RB_OK;
 }
@@ -944,7 +987,7 @@ extern "C" {
 int multibody_kernel_path_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled) {
     if (int rc = check_kernel_query(mb, kind, batch)) return -rc;
     if (resolve_kernel(mb, kind, f64 != 0, batch, tiled != 0)) return 1;
-    if (rbamd::jit_enabled() && !(kind >= 4 && kin_precompiled(mb))) note_jit_errors(mb);
+    if (rbamd::jit_enabled() && !((kind == 4 || kind == 5) && kin_precompiled(mb))) note_jit_errors(mb);
     return 0;
 }
 
@@ -1084,6 +1127,25 @@ int multibody_fd_batch_tiled_f32(const Multibody *mb, const float *q, const floa
 int multibody_fd_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
                                  double *qdd, int64_t batch, void *stream) {
     return fd_batch<double>(mb, q, qd, tau, qdd, batch, 256, stream, true);
+}
+int multibody_rnea_fd_batch_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                const float *tau_in, float *tau, float *qdd_out, int64_t batch, int64_t ld,
+                                void *stream) {
+    return idfd_batch<float>(mb, q, qd, qdd, tau_in, tau, qdd_out, batch, ld, stream);
+}
+int multibody_rnea_fd_batch_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                const double *tau_in, double *tau, double *qdd_out, int64_t batch, int64_t ld,
+                                void *stream) {
+    return idfd_batch<double>(mb, q, qd, qdd, tau_in, tau, qdd_out, batch, ld, stream);
+}
+int multibody_rnea_fd_batch_tiled_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                      const float *tau_in, float *tau, float *qdd_out, int64_t batch, void *stream) {
+    return idfd_batch<float>(mb, q, qd, qdd, tau_in, tau, qdd_out, batch, 256, stream, true);
+}
+int multibody_rnea_fd_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                      const double *tau_in, double *tau, double *qdd_out, int64_t batch,
+                                      void *stream) {
+    return idfd_batch<double>(mb, q, qd, qdd, tau_in, tau, qdd_out, batch, 256, stream, true);
 }
 int multibody_rollout_batch_f32(const Multibody *mb, float *q, float *qd, const float *tau_seq, double dt, int K,
                                  float *traj, int64_t batch, int64_t ld, void *stream) {

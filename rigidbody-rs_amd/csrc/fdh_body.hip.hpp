@@ -141,6 +141,78 @@ RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&loa
     fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) { out(j, gd.out(v)); });
 }
 
+// Inverse AND forward dynamics of one (q, qd) from one set of factors (SURVEY §8(d) config 4's
+// RNEA + forward-dynamics pair; tuning-free, one launch):
+//   tau  = rnea(q, qd, qdd)                       (multibody.rs:111-153)
+//   qdd' = sym(H)^-1 (tau_in - rnea(q, qd, 0))    (the A10 definition above)
+// The RNEA is affine in qdd with slope H (multibody.rs:155-174 computes that H), so
+//   rnea(q, qd, qdd) = C + sym(H) qdd,   C = rnea(q, qd, 0)
+// and the pair shares everything but n^2 FMAs: the bias sweep C and (cos, sin) once, H once
+// (tau accumulates as crba_core emits H's entries, before L D L^T overwrites them), then the
+// factorisation and the solve on tau_in.  Against an RNEA launch followed by a forward-dynamics
+// launch: q and qd are read once (6 n s bytes per configuration instead of 8 n s) and the RNEA's
+// second forward sweep (alpha, a with qdd) is replaced by the n^2 products.
+// Column i of H is complete -- and with it tau_i, whose row entries H[i][k > i] came in the
+// earlier (leaf-side) columns -- when crba_core emits its root entry H[0][i]: tau_i is stored
+// then, leaf first.  Input checks: tau's outputs on (q, qd, qdd), qdd''s on (q, qd, tau_in).
+template <typename T, int N, bool FAST, typename LoadQdd, typename LoadTau, typename OutTau, typename OutQdd>
+RB_HD void fdh_idfd_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], LoadQdd &&load_qdd, LoadTau &&load_tau,
+                         OutTau &&out_tau, OutQdd &&out_qdd) {
+    T cs[N], sn[N], C[N], av[N], tv[N], tau[N], H[N][N], Di[N];
+    InputGuard<T> gd;
+    RB_STAGE("bias_fwd");
+    fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C, gd);
+    load_qdd(av);
+    InputGuard<T> gr = gd;  // tau: q, qd, qdd
+    gr.vals(av);
+#pragma unroll
+    for (int j = 0; j < N; ++j) tau[j] = C[j];
+    reload_fence();
+    RB_STAGE("crba");
+    crba_core<T, N>(mdl, cs, sn, [&](int e, T v) {
+        const int j = e % N, i = e / N;
+        if (j > i) return;  // the strictly-lower zeros
+        H[j][i] = v;
+        tau[j] = fmadd(v, av[i], tau[j]);
+        if (j < i) tau[i] = fmadd(v, av[j], tau[i]);
+        if (j == 0) out_tau(i, gr.out(tau[i]));
+    });
+    load_tau(tv);
+    RB_STAGE("ldl");
+    fdh_ldl<T, N>(H, Di);
+    InputGuard<T> gf = gd;  // qdd': q, qd, tau_in
+    gf.vals(tv);
+    RB_STAGE("solve");
+    fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) { out_qdd(j, gf.out(v)); });
+}
+
+// Lane body of the pair: q, qd rows in first-use order, qdd after the bias sweep, tau_in after
+// the mass matrix (it enters at the solve).
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void idfd_lane(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                          const T *__restrict__ qdd, const T *__restrict__ tau_in,
+                                          T *__restrict__ tau, T *__restrict__ qdd_out, uint32_t b, int64_t ld) {
+    const uint32_t off = b * (uint32_t)sizeof(T);
+    T qv[N], qdv[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        qv[j] = ld_row(q, j * ld, off);
+        __builtin_amdgcn_sched_barrier(0);
+        qdv[j] = ld_row(qd, j * ld, off);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    auto rows = [&](const T *__restrict__ src, T (&v)[N]) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            v[j] = ld_row(src, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    fdh_idfd_eval<T, N, FAST>(
+        mdl, qv, qdv, [&](T (&v)[N]) { rows(qdd, v); }, [&](T (&v)[N]) { rows(tau_in, v); },
+        [&](int j, T v) { st_row(tau, j * ld, off, v); }, [&](int j, T v) { st_row(qdd_out, j * ld, off, v); });
+}
+
 // Kinematic trees (Topo, tree_body.hip.hpp): the same definition with the tree forms of its
 // stages -- bias torques by rnea_eval_tree at qdd = 0, H by crba_eval_tree (exact zeros for
 // joint pairs that are not ancestor / descendant), then the same L D L^T and solves.  Each stage

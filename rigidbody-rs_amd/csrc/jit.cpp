@@ -46,7 +46,7 @@ std::string literal(double x, bool f64) {
 
 int jit_nt(JitKind kind) {
     if (kind == JitKind::Rnea) return tuning().rnea_nt < 0 ? 3 : (tuning().rnea_nt & 3);
-    if (kind == JitKind::Fd || kind == JitKind::Rollout) return tuning().fd_nt & 3;
+    if (kind == JitKind::Fd || kind == JitKind::Rollout || kind == JitKind::RneaFd) return tuning().fd_nt & 3;
     const int v = tuning().kin_nt;  // CRBA, fwd_kin, jac
     if (v >= 0) return v & 3;
     return kind == JitKind::FwdKin ? 3 : 2;  // 7 rows in / 3 out: non-temporal loads pay too
@@ -173,7 +173,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     }
     const char *F = fast ? "true" : "false";
     const int pack = jit_model_pack(m, kind, f64, pack_req);
-    const bool fdh = kind == JitKind::Fd && jit_fd_form(m) == 2;
+    const bool fdh = (kind == JitKind::Fd || kind == JitKind::RneaFd) && jit_fd_form(m) == 2;
     std::ostringstream o;
     o << "#define RB_NT " << (nt >= 0 ? nt : jit_nt(kind)) << "\n";
     o << "#define RB_VARIANT " << tuning().jit_variant << "\n";
@@ -225,7 +225,7 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
     // memory-bound headline kernel gains nothing from fewer VALU, its sequential pair would need
     // 131 instead of 125 VGPRs (3 waves/SIMD instead of 4), and all its grid forms (pairs,
     // single tail, one per lane below 2^19) must stay bit-identical to each other.
-    const bool dyn = kind == JitKind::Rnea || kind == JitKind::Fd || kind == JitKind::Rollout;
+    const bool dyn = kind == JitKind::Rnea || kind == JitKind::Fd || kind == JitKind::Rollout || kind == JitKind::RneaFd;
     // jit_variant bit 16384 (A/B): the centre-of-mass form for the fp64 RNEA too
     // rnea_lane_rev: the fp64 RNEA of serial chains longer than 8 links, whose per-link forces
     // hold one wave per SIMD (12 links 264 VGPRs, 30 links 496) and do not fit LDS either
@@ -383,6 +383,16 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << "  if (b >= B) return;\n";
         o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
         o << "  rbamd::dev::rnea_lane<T, N, " << F << ", Topo>(kModel, q + o, qd + o, qdd + o, tau + o, threadIdx.x, ld);\n}\n";
+    } else if (kind == JitKind::RneaFd) {
+        // one configuration per lane; the launcher takes this kind only for mass-matrix models
+        o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
+             "const T *__restrict__ qdd, const T *__restrict__ tau_in, T *__restrict__ tau, "
+             "T *__restrict__ qdd_out, uint32_t B, int64_t ld, int64_t bs) {\n";
+        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+        o << "  if (b >= B) return;\n";
+        o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+        o << "  rbamd::dev::idfd_lane<T, N, " << F
+          << ">(kModel, q + o, qd + o, qdd + o, tau_in + o, tau + o, qdd_out + o, threadIdx.x, ld);\n}\n";
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";

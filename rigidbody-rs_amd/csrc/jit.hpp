@@ -25,7 +25,10 @@ namespace rbamd {
 
 // FwdKin / Jac: built only for models the precompiled kinematics kernels cannot express
 // (kinematic trees, prismatic joints -- Model::serial_revolute() false).
-enum class JitKind : int { Rnea = 0, Fd = 1, Crba = 2, Rollout = 3, FwdKin = 4, Jac = 5 };
+// RneaFd: inverse + forward dynamics of the same (q, qd) in one launch (fdh_body.hip.hpp
+// fdh_idfd_eval), for models on the mass-matrix forward dynamics (jit_fd_form 2).
+enum class JitKind : int { Rnea = 0, Fd = 1, Crba = 2, Rollout = 3, FwdKin = 4, Jac = 5, RneaFd = 6 };
+constexpr int kJitKinds = 7;
 
 struct JitKernel {
     hipModule_t module = nullptr;

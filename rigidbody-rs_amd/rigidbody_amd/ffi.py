@@ -78,6 +78,8 @@ for _t in ("f32", "f64"):
     _sig(f"multibody_fd_batch_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp])
     _sig(f"multibody_crba_batch_{_t}", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
     _sig(f"rb_fill_uniform_{_t}", ctypes.c_int, [_vp, ctypes.c_int, _i64, _i64, _dp, _dp, ctypes.c_uint64, _vp])
+    _sig(f"multibody_rnea_fd_batch_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp])
+    _sig(f"multibody_rnea_fd_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp])
 _sig("multibody_fwd_kin_batch_f64", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_fwd_kin_batch_f32", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
 _sig("multibody_jac_batch_f32", ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp])
@@ -95,7 +97,7 @@ _sig("multibody_jit_source", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, cty
 _sig("multibody_jit_compile", _i64, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p])
 _sig("multibody_jit_source_ex", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _i64, ctypes.c_int, ctypes.c_char_p, _i64])
 _sig("multibody_jit_compile_ex", _i64, [_vp, ctypes.c_int, ctypes.c_int, _i64, ctypes.c_int, ctypes.c_char_p])
-KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3, "fwd_kin": 4, "jac": 5}
+KINDS = {"rnea": 0, "fd": 1, "crba": 2, "rollout": 3, "fwd_kin": 4, "jac": 5, "rnea_fd": 6}
 GENERAL_AXES, URDF_TREE, FLOATING_BASE = 1, 2, 4  # rigidbody_batch.h RB_MODEL_*
 _ip = ctypes.POINTER(ctypes.c_int)
 _sig("multibody_topology", ctypes.c_int, [_vp, _ip, _ip])
@@ -417,6 +419,36 @@ class Multibody:
             _check(fn(self._h, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), out.data_ptr(), B, ld,
                       _stream_ptr(stream, dev)), "fd_batch")
         return out
+
+    def rnea_fd_batch(self, q, qd, qdd, tau_in, tau=None, qdd_out=None, stream=None):
+        """multibody_rnea_fd_batch_*: (tau = rnea(q, qd, qdd), qdd_out = fd(q, qd, tau_in)) in one
+        launch for mass-matrix models (two kernels otherwise); [n, B] CUDA tensors."""
+        q = _soa(q, self.n, "q")
+        B = q.shape[1]
+        ins = [q] + [_soa(x, self.n, k, q.dtype, B) for x, k in ((qd, "qd"), (qdd, "qdd"), (tau_in, "tau_in"))]
+        outs = []
+        for o, k in ((tau, "tau"), (qdd_out, "qdd_out")):
+            o = torch.empty_strided(q.shape, q.stride(), dtype=q.dtype, device=q.device) if o is None else o
+            outs.append(_soa(o, self.n, k, q.dtype, B))
+        ld = _same_ld(ins + outs)
+        dev = _one_device(ins + outs)
+        fn = getattr(_lib, f"multibody_rnea_fd_batch_{_TORCH_SUFFIX[q.dtype]}")
+        with torch.cuda.device(dev):
+            _check(fn(self._h, *[t.data_ptr() for t in ins + outs], B, ld, _stream_ptr(stream, dev)), "rnea_fd_batch")
+        return outs[0], outs[1]
+
+    def rnea_fd_batch_tiled(self, q, qd, qdd, tau_in, B, tau=None, qdd_out=None, stream=None):
+        """The same on tiled [ceil(B/256), n, 256] tensors (multibody_rnea_fd_batch_tiled_*)."""
+        q = self._tiled(q, "q", B)
+        ins = [q] + [self._tiled(x, k, B, q.dtype) for x, k in ((qd, "qd"), (qdd, "qdd"), (tau_in, "tau_in"))]
+        outs = [torch.empty_like(q) if o is None else self._tiled(o, k, B, q.dtype)
+                for o, k in ((tau, "tau"), (qdd_out, "qdd_out"))]
+        dev = _one_device(ins + outs)
+        fn = getattr(_lib, f"multibody_rnea_fd_batch_tiled_{_TORCH_SUFFIX[q.dtype]}")
+        with torch.cuda.device(dev):
+            _check(fn(self._h, *[t.data_ptr() for t in ins + outs], B, _stream_ptr(stream, dev)),
+                   "rnea_fd_batch_tiled")
+        return outs[0], outs[1]
 
     # ---- tiled layout [ceil(B/256), n, 256] (rigidbody_batch.h) ----------------------
     def _tiled(self, t, name, B, dtype=None):

@@ -135,34 +135,33 @@ def test_config3_fd_f32_b65536(ffi, dev, fr3_text):
 # ------------------------------------------------------------------ config 4
 def test_config4_rnea_fd_f64(ffi, dev, fr3_text):
     """Config 4: fr3 RNEA + forward dynamics, fp64, on the global 2^20 batch and on one GPU's
-    2^17 shard of it (N = 8): tau = rnea(q, qd, qdd) against the oracle, then fd(q, qd, tau)
-    with the oracle's torque residual and the fd . rnea round trip.  The shard is the first 2^17
-    configurations of the 2^20 draw, launched on its own: it must equal those columns of the
-    full launch bit for bit (the RNEA's grid forms share one lane body; so do the FD's when
-    both sizes take the same form)."""
+    2^17 shard of it (N = 8).  The pair as bench.py times it -- multibody_rnea_fd_batch_tiled_f64,
+    tau = rnea(q, qd, qdd) and qdd' = fd(q, qd, tau_in) in one launch -- against the oracle (tau
+    1e-9 scaled, qdd' by its torque residual 1e-8), and the chained separate calls
+    (fd(q, qd, rnea(q, qd, qdd)) = qdd, round trip).  The shard is the first 2^17 configurations
+    of the 2^20 draw, launched on its own: bit for bit those columns of the full launch."""
     from rigidbody_amd import chains
 
     G, S = 1 << 20, 1 << 17
     mb = ffi.Multibody.new()
-    q, qd, qdd = _draw(ffi, mb, ("q", "qd", "qdd"), G, torch.float64, chains.SEED)
+    assert mb.kernel_path("rnea_fd", True, G, True) == "jit" and mb.kernel_path("rnea_fd", True, S, True) == "jit"
+    q, qd, qdd, tin = _draw(ffi, mb, ("q", "qd", "qdd", "tau"), G, torch.float64, chains.SEED)
     om = _oracle(fr3_text)
-    h = [x.cpu().numpy() for x in (q, qd, qdd)]
+    h = [x.cpu().numpy() for x in (q, qd, qdd, tin)]
+    t = [ffi.to_tiled(x) for x in (q, qd, qdd, tin)]
+    tau_f, qdd_f = (ffi.from_tiled(o, G) for o in mb.rnea_fd_batch_tiled(*t, G))
+    tau_h, qddf_h = tau_f.cpu().numpy(), qdd_f.cpu().numpy()
+    assert _scaled(tau_h, om.rnea_batch(*h[:3], nthreads=ORACLE_THREADS)) <= 1e-9
+    res = om.rnea_batch(h[0], h[1], qddf_h, nthreads=ORACLE_THREADS) - h[3]
+    assert np.all(np.isfinite(qddf_h)) and (np.abs(res) / (1 + np.abs(h[3]))).max() <= 1e-8
+    # the shard on its own
+    tau_s, qdd_s = (ffi.from_tiled(o, S) for o in mb.rnea_fd_batch_tiled(*[x[: S // 256].contiguous() for x in t], S))
+    assert torch.equal(tau_s, tau_f[:, :S]) and torch.equal(qdd_s, qdd_f[:, :S])
+    # the separate calls, chained: fd . rnea = identity up to the conditioning of H
     tau = _tiled(ffi, mb, "rnea", (q, qd, qdd), G)
-    qdd2 = _tiled(ffi, mb, "fd", (q, qd, tau), G)
-    tau_h, qdd2_h = tau.cpu().numpy(), qdd2.cpu().numpy()
-    assert _scaled(tau_h, om.rnea_batch(*h, nthreads=ORACLE_THREADS)) <= 1e-9
-    res = om.rnea_batch(h[0], h[1], qdd2_h, nthreads=ORACLE_THREADS) - tau_h
-    assert (np.abs(res) / (1 + np.abs(tau_h))).max() <= 1e-8
-    # fd . rnea = identity up to the conditioning of H
-    assert _scaled(qdd2_h, h[2]) <= 1e-7
-    sh = [x[:, :S].contiguous() for x in (q, qd, qdd)]
-    tau_s = _tiled(ffi, mb, "rnea", sh, S)
-    qdd_s = _tiled(ffi, mb, "fd", (sh[0], sh[1], tau_s), S)
-    assert torch.equal(tau_s, tau[:, :S])
-    if mb.kernel_form("fd", True, S, True) == mb.kernel_form("fd", True, G, True):
-        assert torch.equal(qdd_s, qdd2[:, :S])
-    else:  # a different grid form of the same definition
-        assert _scaled(qdd_s.cpu().numpy(), qdd2_h[:, :S]) <= 1e-9
+    back = _tiled(ffi, mb, "fd", (q, qd, tau), G).cpu().numpy()
+    assert _scaled(back, h[2]) <= 1e-7
+    assert _scaled(tau_h, tau.cpu().numpy()) <= 1e-9
 
 
 # ------------------------------------------------------------------ config 5

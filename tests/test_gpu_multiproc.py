@@ -54,24 +54,31 @@ WORKER = textwrap.dedent('''
     q, qd, qdd = (torch.as_tensor(a, device=dev) for a in x)
     tau = mb.rnea_batch(q, qd, qdd)          # multibody_rnea_batch_f64 on the shard
     back = mb.fd_batch(q, qd, tau)           # multibody_fd_batch_f64 on its torques
+    # the same pair in one fused launch (multibody_rnea_fd_batch_f64, tau_in = the RNEA's torques)
+    ftau, fback = mb.rnea_fd_batch(q, qd, qdd, tau)
     torch.cuda.synchronize()
     parts = [None] * world
-    dist.all_gather_object(parts, (b0, b1, tau.cpu().numpy(), back.cpu().numpy()))
+    dist.all_gather_object(parts, (b0, b1, tau.cpu().numpy(), back.cpu().numpy(), ftau.cpu().numpy(),
+                                   fback.cpu().numpy()))
     out = {{"rank": rank, "shard": [b0, b1], "kernel_path": [mb.kernel_path("rnea", True), mb.kernel_path("fd", True)]}}
     if rank == 0:
         from oracle import oracle, urdf_model
         full = [chains.host_uniform(7, G, *chains.input_ranges(lim, k), chains.SEED + 60 + i)
                 for i, k in enumerate(("q", "qd", "qdd"))]
-        T = np.zeros((7, G)); Q = np.zeros((7, G))
+        T = np.zeros((7, G)); Q = np.zeros((7, G)); FT = np.zeros((7, G)); FQ = np.zeros((7, G))
         cover = np.zeros(G, int)
-        for p0, p1, t, bq in parts:
-            T[:, p0:p1] = t; Q[:, p0:p1] = bq; cover[p0:p1] += 1
+        for p0, p1, t, bq, ft, fq_ in parts:
+            T[:, p0:p1] = t; Q[:, p0:p1] = bq; FT[:, p0:p1] = ft; FQ[:, p0:p1] = fq_; cover[p0:p1] += 1
         assert (cover == 1).all(), "shards must tile the batch exactly once"
         fq, fqd, fqdd = (torch.as_tensor(a, device=dev) for a in full)
         T1 = mb.rnea_batch(fq, fqd, fqdd).cpu().numpy()
         Q1 = mb.fd_batch(fq, fqd, torch.as_tensor(T1, device=dev)).cpu().numpy()
         out["bit_identical_tau"] = bool(np.array_equal(T, T1))
         out["bit_identical_fd"] = bool(np.array_equal(Q, Q1))
+        FT1, FQ1 = (o.cpu().numpy() for o in mb.rnea_fd_batch(fq, fqd, fqdd, torch.as_tensor(T1, device=dev)))
+        out["bit_identical_fused"] = bool(np.array_equal(FT, FT1) and np.array_equal(FQ, FQ1))
+        out["fused_fd_equals_fd"] = bool(np.array_equal(FQ, Q))
+        out["fused_tau_vs_rnea"] = float((np.abs(FT - T) / (1 + np.abs(T))).max())
         out["round_trip"] = float((np.abs(Q - full[2]) / (1 + np.abs(full[2]))).max())
         om = oracle.Model(urdf_model.model_raw_from_urdf(chains.fr3_urdf_text()))
         idx = np.linspace(0, G - 1, 1024).astype(int)
@@ -108,6 +115,7 @@ def test_two_ranks_shard_rnea_fd_f64(tmp_path):
     assert [o["shard"] for o in outs] == [[0, (G + 1) // 2], [(G + 1) // 2, G]]
     assert all(o["kernel_path"] == ["jit", "jit"] for o in outs)
     assert r0["bit_identical_tau"] and r0["bit_identical_fd"], r0
+    assert r0["bit_identical_fused"] and r0["fused_fd_equals_fd"] and r0["fused_tau_vs_rnea"] <= 1e-9, r0
     assert r0["round_trip"] <= 1e-8, r0
     assert r0["oracle_tau"] <= 1e-9, r0
 
@@ -124,7 +132,7 @@ def test_bench_two_ranks_strong_rnea_fd():
     assert compact["value"] == line["value"] and len(compact["per_rank"]) == 2
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["config"]["global_batch"] == 1 << 18 and line["config"]["batch_per_gpu"] == 1 << 17
-    assert line["value"] > 0 and line["config"]["kernel_path"] == "jit+jit"
+    assert line["value"] > 0 and line["config"]["kernel_path"] == "jit"
     assert [x["rank"] for x in line["per_rank"]] == [0, 1] and all(x["kernel_ms_avg"] > 0 for x in line["per_rank"])
 
 
@@ -149,7 +157,7 @@ def test_bench_two_ranks_weak_with_strong_split():
     # SURVEY §8(d) config 4 in the N > 1 line: RNEA + FD fp64 on shards of one global 2^20 batch,
     # both hipRTC kernels, its own budget, per-rank times
     c4 = line["secondary"]["strong_split_rnea_fd"]
-    assert c4["kernel_path"] == "jit+jit" and c4["dtype"] == "f64"
+    assert c4["kernel_path"] == "jit" and c4["dtype"] == "f64"
     assert c4["global_batch"] == bench.CONFIG4_BATCH and c4["batch_per_gpu_max"] == bench.CONFIG4_BATCH // 2
     assert c4["launches"] >= bench.SIDE_MIN_LAUNCHES and [x["steps"] for x in c4["per_rank"]] == [c4["launches"]] * 2
     assert c4["pairs_per_s"] > 0 and 0 < c4["hbm_frac_max_rank"] <= 1 and c4["graph_pairs_per_s"] > 0
