@@ -158,8 +158,10 @@ int multibody_kernel_form_ex(const Multibody *mb, int kind, int f64, int64_t bat
 int multibody_single_config_path(const Multibody *mb);
 /* The generated source of the model-specialised kernel a launch of `batch` configurations
  * (tiled != 0: the *_tiled entry points) runs -- the same form, tail and load / store policy
- * multibody_kernel_form_ex reports; returns its length; copies at most cap-1 bytes + NUL into
- * buf when buf != NULL.  multibody_jit_source = a 2^20-configuration SoA launch. */
+ * multibody_kernel_form_ex reports, and the occupancy target the occupancy-cliff rebuild adds
+ * (the source is hipRTC-compiled for gfx950 to decide it, no device needed); returns its length;
+ * copies at most cap-1 bytes + NUL into buf when buf != NULL.  multibody_jit_source = a
+ * 2^20-configuration SoA launch. */
 int multibody_jit_source_ex(const Multibody *mb, int kind, int f64, int64_t batch, int tiled, char *buf,
                             int64_t cap);
 int multibody_jit_source(const Multibody *mb, int kind, int f64, char *buf, int64_t cap);

@@ -965,14 +965,27 @@ void resolve_pack(const Multibody *mb, rbamd::JitKind kind, bool f64, const JitS
     *tl = (kind == rbamd::JitKind::Rnea && *pk == 3) ? sh.tail : 0;
 }
 
-// The hipRTC source of the kernel a launch of `batch` configurations (tiled or SoA) would run.
+// The hipRTC source of the kernel a launch of `batch` configurations (tiled or SoA) would run:
+// compiled here (hipRTC, gfx950, no device needed) so that the occupancy-cliff rebuild of
+// jit_compile shows in it -- the source of the code object a launch really loads; the generated
+// source as it stands if hipRTC fails.
 std::string shaped_source(const Multibody *mb, int kind, bool f64, int64_t batch, bool tiled) {
     const uint32_t B = batch < kChunk ? (uint32_t)batch : (uint32_t)kChunk;
     const auto k = (rbamd::JitKind)kind;
     const JitShape sh = jit_shape(mb, k, f64, B, tiled);
     int pk = 0, tl = 0;
     resolve_pack(mb, k, f64, sh, &pk, &tl);
-    return rbamd::jit_source(mb->model, k, f64, sh.fast, pk, tl, sh.nt);
+    // the length query and the copy of multibody_jit_source_ex come in pairs: one compile for both
+    thread_local std::string t_key, t_src;
+    const std::string plain = rbamd::jit_source(mb->model, k, f64, sh.fast, pk, tl, sh.nt);
+    const std::string key = std::to_string((uintptr_t)mb) + ":" + std::to_string(rbamd::tuning_generation()) + ":" + plain;
+    if (key == t_key) return t_src;
+    std::vector<char> code;
+    std::string err, src;
+    if (!rbamd::jit_compile(mb->model, k, f64, sh.fast, "gfx950", &code, &err, pk, tl, sh.nt, &src)) src = plain;
+    t_key = key;
+    t_src = src;
+    return src;
 }
 
 void note_jit_errors(const Multibody *mb) {

@@ -44,10 +44,10 @@ RB_HD void fdh_bias(const T *mdl, const T (&qv)[N], const T (&qdv)[N], T (&cs)[N
                     InputGuard<T> &gd) {
     V3<T> fn[N], ff[N];  // ff: the link force, or g = f / m (kRneaGForm)
     RneaState<T> st;
-    rnea_fwd0<T, FAST, kRneaGForm>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0], gd);
+    rnea_fwd0<T, FAST, kRneaGForm, false>(mdl, qv[0], qdv[0], T(0), st, sn[0], cs[0], fn[0], ff[0], gd);
 #pragma unroll
     for (int j = 1; j < N; ++j)
-        rnea_fwd<T, FAST, kRneaGForm>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j], gd);
+        rnea_fwd<T, FAST, kRneaGForm, false>(mdl, j, qv[j], qdv[j], T(0), st, sn[j], cs[j], fn[j], ff[j], gd);
     reload_fence();
     RB_STAGE("bias_bwd");
     if constexpr (kRneaGForm) {

@@ -503,7 +503,7 @@ bool rtc_compile(const std::string &src, const std::string &arch, bool no_licm, 
 }  // namespace
 
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
-                 std::vector<char> *code, std::string *error, int pack, int tail, int nt) {
+                 std::vector<char> *code, std::string *error, int pack, int tail, int nt, std::string *final_src) {
     std::string src = jit_source(m, kind, f64, fast, pack, tail, nt);
     // The paired fp32 rollout and the fp64 rollout of short chains keep 2 waves/SIMD only
     // without machine LICM: hoisting per-step address arithmetic and constants out of the K
@@ -523,6 +523,7 @@ bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::s
             }
         }
     }
+    if (final_src) *final_src = src;
     // RB_JIT_DUMP=dir: keep every compiled source and code object for inspection
     // (llvm-objdump / llvm-readelf on the .co: registers, scratch, ISA of what really runs)
     if (const char *dir = std::getenv("RB_JIT_DUMP")) {

@@ -76,9 +76,11 @@ int jit_seq_tail(bool tiled);
 // wave per SIMD, <= 16 over) is rebuilt with a 2-wave target -- a few spilled values cost less
 // than half the SIMD's waves (the 9-joint tree's fp64 RNEA: 258 registers; 65.0 vs 92.9 us at
 // 2^20 with 12 B of scratch).
+// final_src (optional): the source of the code object returned -- the occupancy-cliff rebuild's
+// when that rule applied (multibody_jit_source_ex reports this one).
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,
                  std::vector<char> *code, std::string *error, int pack = 0, int tail = 0,
-                 int nt = -1);
+                 int nt = -1, std::string *final_src = nullptr);
 
 // Compiles and loads the kernel on the current device.  Never throws.
 JitKernel jit_build(const Model &m, JitKind kind, bool f64, bool fast, int pack = 0, int tail = 0, int nt = -1);

@@ -27,13 +27,15 @@ struct RneaState {
 #ifndef RB_GUARD_ANCHOR
 #define RB_GUARD_ANCHOR 0
 #endif
-template <typename T, bool FAST, bool GF = false>
+// QDD = false: qdd is the constant 0 of a bias sweep (fdh_bias), nothing to check (the guard's
+// asm FMA would not fold away on it, spatial.hip.hpp InputGuard).
+template <typename T, bool FAST, bool GF = false, bool QDD = true>
 RB_HD void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn, T &cs,
                                           V3<T> &fn, V3<T> &ff, InputGuard<T> &gd) {
     const Link<T> L = load_link(mdl, 0);
     gd.angle(q0);
     gd.val(qd0);
-    gd.val(qdd0);
+    if constexpr (QDD) gd.val(qdd0);
     sin_cos<FAST>(q0, sn, cs);
     const M3<T> E = joint_rotation(L.Rp, cs, sn);
     const T g = T(kGravity);
@@ -51,13 +53,13 @@ RB_HD void rnea_fwd0(const T *mdl, T q0, T qd0, T qdd0, RneaState<T> &st, T &sn,
 }
 
 // Link j >= 1: forward sweep step (multibody.rs:122-141).
-template <typename T, bool FAST, bool GF = false>
+template <typename T, bool FAST, bool GF = false, bool QDD = true>
 RB_HD void rnea_fwd(const T *mdl, int j, T qj, T qdj, T qddj, RneaState<T> &st, T &sn, T &cs,
                                          V3<T> &fn, V3<T> &ff, InputGuard<T> &gd) {
     const Link<T> L = load_link(mdl, j);
     gd.angle(qj);
     gd.val(qdj);
-    gd.val(qddj);
+    if constexpr (QDD) gd.val(qddj);
     sin_cos<FAST>(qj, sn, cs);
     const M3<T> E = joint_rotation(L.Rp, cs, sn);
     // SpatialVelocity::transform (spatial.rs:110-116) on v and a

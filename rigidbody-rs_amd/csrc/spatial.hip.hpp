@@ -606,6 +606,21 @@ __device__ __forceinline__ f2 recip(f2 x) { return f2{__builtin_amdgcn_rcpf(x.x)
 // On the host (the single-configuration ABI) angles are checked for Inf / NaN only: sincos_cw
 // falls back to the C library past 2^45, so every finite angle is in range there, as in the
 // reference.
+//
+// Out of the optimizer's reach.  The model-specialised kernels compile under
+// -ffinite-math-only, where LLVM may treat the NaN of an nnan operation, or the Inf of an ninf
+// one, as poison -- and may fold a bit test on such a value (e.g. into is.fpclass of a value
+// "known" not to be NaN).  So on the device every step of the check is an instruction the
+// compiler cannot see into: the scaled angle (v_mul), the accumulation (v_fma, z an SGPR) and
+// the output add (fp32) are inline assembly, and fp64 outputs test acc's bits shifted by an asm
+// v_lshlrev (an integer of unknown origin, not a bitcast of a float).  Same instructions, same
+// count as the plain arithmetic; each carries the assembly comment "rb_guard" so a test can
+// count them in the ISA (tests/test_boundary.py).
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
+#define RB_GUARD_ASM 1
+#else
+#define RB_GUARD_ASM 0
+#endif
 RB_HD float guard_view(float x) { return x; }
 RB_HD f2 guard_view(f2 x) { return x; }
 RB_HD float guard_view(double x) {
@@ -617,6 +632,74 @@ RB_HD f2 angle_scale(f2) { return f2{0x1p106f, 0x1p106f}; }
 RB_HD float guard_acc(double) { return 0.0f; }
 RB_HD float guard_acc(float) { return 0.0f; }
 RB_HD f2 guard_acc(f2) { return f2{0.0f, 0.0f}; }
+
+// acc + v z
+RB_HD float guard_fma(float v, float z, float acc) {
+#if RB_GUARD_ASM
+    asm("v_fma_f32 %0, %1, %2, %0 ; rb_guard" : "+v"(acc) : "v"(v), "s"(z));
+    return acc;
+#else
+    return __builtin_fmaf(v, z, acc);
+#endif
+}
+RB_HD f2 guard_fma(f2 v, f2 z, f2 acc) {
+#if RB_GUARD_ASM
+    asm("v_pk_fma_f32 %0, %1, %2, %0 ; rb_guard" : "+v"(acc) : "v"(v), "s"(z));
+    return acc;
+#else
+    return fmadd(v, z, acc);
+#endif
+}
+// v * scale (Inf past the angle bound)
+RB_HD float guard_scale(float v, float sc) {
+#if RB_GUARD_ASM
+    float r;  // a fresh register: v (the angle's high word) lives on for the sincos
+    asm("v_mul_f32 %0, %1, %2 ; rb_guard" : "=v"(r) : "s"(sc), "v"(v));
+    return r;
+#else
+    return v * sc;
+#endif
+}
+RB_HD f2 guard_scale(f2 v, f2 sc) {
+#if RB_GUARD_ASM
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 ; rb_guard" : "=v"(r) : "s"(sc), "v"(v));
+    return r;
+#else
+    return v * sc;
+#endif
+}
+// y + acc
+RB_HD float guard_add(float y, float acc) {
+#if RB_GUARD_ASM
+    float r;
+    asm("v_add_f32 %0, %1, %2 ; rb_guard" : "=v"(r) : "v"(acc), "v"(y));
+    return r;
+#else
+    return y + acc;
+#endif
+}
+RB_HD f2 guard_add(f2 y, f2 acc) {
+#if RB_GUARD_ASM
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 ; rb_guard" : "=v"(r) : "v"(acc), "v"(y));
+    return r;
+#else
+    return y + acc;
+#endif
+}
+// acc's bits shifted left by one (the sign dropped) as an integer the compiler knows nothing
+// about: the shift the NaN test needs anyway, issued as asm, so the test below cannot be
+// recognised as an is-NaN test of a float (which no-nans-fp-math would fold to false).
+RB_HD uint32_t guard_bits2(float acc) {
+#if RB_GUARD_ASM
+    uint32_t t;
+    asm("v_lshlrev_b32 %0, 1, %1 ; rb_guard" : "=v"(t) : "v"(acc));
+    return t;
+#else
+    return __builtin_bit_cast(uint32_t, acc) << 1;
+#endif
+}
 
 template <typename T>
 struct InputGuard {
@@ -631,12 +714,13 @@ struct InputGuard {
     // RB_VARIANT bit 2048 (A/B only): no checks -- the round-4 kernels' arithmetic
     static constexpr bool kOff = (RB_VARIANT & 2048) != 0;
     RB_HD void val(T x) {
-        if constexpr (!kOff) acc = fmadd(guard_view(x), z, acc);
+        if constexpr (!kOff) acc = guard_fma(guard_view(x), z, acc);
     }
     RB_HD void angle(T x) {
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
         // bit 8192 (A/B only): no angle checks (rows the dynamics never read stay unread)
-        if constexpr (!kOff && (RB_VARIANT & 8192) == 0) acc = fmadd(guard_view(x) * angle_scale(x), z, acc);
+        if constexpr (!kOff && (RB_VARIANT & 8192) == 0)
+            acc = guard_fma(guard_scale(guard_view(x), angle_scale(x)), z, acc);
 #else
         val(x);
 #endif
@@ -665,10 +749,10 @@ struct InputGuard {
         if constexpr (kOff) {
             return y;
         } else if constexpr (__is_same(T, double)) {
-            const uint32_t m = (__builtin_bit_cast(uint32_t, acc) << 1) > 0xff000000u ? 0x7ff80000u : 0u;
+            const uint32_t m = guard_bits2(acc) > 0xff000000u ? 0x7ff80000u : 0u;
             return __builtin_bit_cast(T, __builtin_bit_cast(uint64_t, y) | ((uint64_t)m << 32));
         } else {
-            return y + acc;
+            return guard_add(y, acc);
         }
     }
 };

@@ -128,7 +128,7 @@ def test_rnea_fd_other_models(ffi, dev, model):
     from rigidbody_amd import chains
 
     if model == "tree9":
-        mb = ffi.Multibody.from_urdf_string(chains.tree_urdf(), ffi.URDF_TREE)
+        mb = ffi.Multibody.from_urdf_string(chains.tree_urdf(), ffi.URDF_TREE | ffi.GENERAL_AXES)
     else:
         mb = ffi.Multibody.from_urdf_string(chains.synthetic_chain_urdf(int(model[5:])))
     fused = model == "chain12"
