@@ -324,12 +324,15 @@ const rbamd::JitKernel *jit_rollout(const Multibody *mb, bool f64, uint32_t B) {
     return jit_shaped(mb, rbamd::JitKind::Rollout, f64, B, false);
 }
 
+int idfd_pack(bool f64, uint32_t B);
+
 JitShape jit_shape(const Multibody *mb, rbamd::JitKind kind, bool f64, uint32_t B, bool tiled) {
     JitShape sh;
     switch (kind) {
         case rbamd::JitKind::Rnea: sh = rnea_shape(mb, f64, B, tiled); break;
         case rbamd::JitKind::Fd: sh.pack = fd_pack(mb, f64, B); break;
         case rbamd::JitKind::Rollout: sh.pack = rollout_pack(mb, f64, B); break;
+        case rbamd::JitKind::RneaFd: sh.pack = idfd_pack(f64, B); break;
         default: break;
     }
     // CRBA evaluates its angles with the precise fp32 sincos; every other kind with the fast one
@@ -388,16 +391,28 @@ hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T 
 // (fdh_body.hip.hpp idfd_lane) for models on the mass-matrix forward dynamics; otherwise -- the
 // ABA models (trees, chains over 12 links), hipRTC off or failed -- the RNEA launch then the
 // forward-dynamics launch, the same results.
-const rbamd::JitKernel *jit_idfd(const Multibody *mb, bool f64) {
+// The fused pair's kernel form for B configurations (auto policy when the tuning `pack` is
+// unset): the wave split (pack 5, idfd_split_block1) for fp32 up to 2^16 configurations, one
+// per lane otherwise.  FR3, HIP graph, tiled (profiles/r06/split/): fp32 65536 4.82 vs 5.24 us,
+// 131072 6.79 vs 6.49; fp64 65536 6.64 vs 6.70, 131072 11.55 vs 10.67, 262144 22.06 vs 20.59 --
+// as for the forward dynamics alone (fp64 FD split 10.16 vs 8.62 us at 2^17): the SIMDs already
+// hold 2 waves of the one-per-lane kernel there, and the split repeats the loads and sincos.
+constexpr uint32_t kIdfdSplitMaxBatch32 = 1u << 16;
+int idfd_pack(bool f64, uint32_t B) {
+    if (rbamd::tuning().pack >= 0) return 0;
+    return (!f64 && B <= kIdfdSplitMaxBatch32) ? 5 : 1;
+}
+
+const rbamd::JitKernel *jit_idfd(const Multibody *mb, bool f64, uint32_t B) {
     if (!mb->model.serial_revolute() || rbamd::jit_fd_form(mb->model, rbamd::JitKind::RneaFd) != 2) return nullptr;
-    return jit_get(mb, rbamd::JitKind::RneaFd, f64, !f64 && fast_trig());
+    return jit_shaped(mb, rbamd::JitKind::RneaFd, f64, B, false);
 }
 
 template <typename T>
 hipError_t launch_idfd_any(const Multibody *mb, const T *mdl, const T *q, const T *qd, const T *qdd, const T *tau_in,
                            T *tau, T *qdd_out, uint32_t B, int64_t ld, hipStream_t s, bool tiled = false) {
     if (B == 0) return hipSuccess;
-    if (const rbamd::JitKernel *jk = jit_idfd(mb, sizeof(T) == 8)) {
+    if (const rbamd::JitKernel *jk = jit_idfd(mb, sizeof(T) == 8, B)) {
         const int64_t lda = tiled ? 256 : ld, bs = tiled ? (int64_t)mb->model.n * 256 : 256;
         void *args[] = {(void *)&q,   (void *)&qd, (void *)&qdd,  (void *)&tau_in, (void *)&tau,
                         (void *)&qdd_out, (void *)&B, (void *)&lda, (void *)&bs};
@@ -947,7 +962,7 @@ const rbamd::JitKernel *resolve_kernel(const Multibody *mb, int kind, bool f64, 
     if (kind == 0) return jit_rnea(mb, f64, B, tiled);
     if (kind == 1) return jit_fd(mb, f64, B);
     if (kind == 3) return jit_rollout(mb, f64, B);
-    if (kind == 6) return jit_idfd(mb, f64);
+    if (kind == 6) return jit_idfd(mb, f64, B);
     if (kind >= 4) return jit_kin(mb, kind == 5, f64);
     return jit_get(mb, rbamd::JitKind::Crba, f64, false);
 }

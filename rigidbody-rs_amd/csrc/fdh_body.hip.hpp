@@ -142,42 +142,56 @@ RB_HD void fdh_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], Tau &&loa
 }
 
 // Inverse AND forward dynamics of one (q, qd) from one set of factors (SURVEY §8(d) config 4's
-// RNEA + forward-dynamics pair; tuning-free, one launch):
+// RNEA + forward-dynamics pair; one launch):
 //   tau  = rnea(q, qd, qdd)                       (multibody.rs:111-153)
 //   qdd' = sym(H)^-1 (tau_in - rnea(q, qd, 0))    (the A10 definition above)
 // The RNEA is affine in qdd with slope H (multibody.rs:155-174 computes that H), so
 //   rnea(q, qd, qdd) = C + sym(H) qdd,   C = rnea(q, qd, 0)
-// and the pair shares everything but n^2 FMAs: the bias sweep C and (cos, sin) once, H once
-// (tau accumulates as crba_core emits H's entries, before L D L^T overwrites them), then the
-// factorisation and the solve on tau_in.  Against an RNEA launch followed by a forward-dynamics
-// launch: q and qd are read once (6 n s bytes per configuration instead of 8 n s) and the RNEA's
-// second forward sweep (alpha, a with qdd) is replaced by the n^2 products.
-// Column i of H is complete -- and with it tau_i, whose row entries H[i][k > i] came in the
-// earlier (leaf-side) columns -- when crba_core emits its root entry H[0][i]: tau_i is stored
-// then, leaf first.  Input checks: tau's outputs on (q, qd, qdd), qdd''s on (q, qd, tau_in).
+// and the pair shares everything but n^2 FMAs: the bias sweep C and (cos, sin) once, H once,
+// then the factorisation and the solve on tau_in.  Against an RNEA launch followed by a
+// forward-dynamics launch: q and qd are read once (6 n s bytes per configuration instead of
+// 8 n s) and the RNEA's own forward sweep with qdd is replaced by the n^2 products.
+// Input checks: tau's outputs on (q, qd, qdd), qdd''s on (q, qd, tau_in).
+
+// h = sym(H) qdd from the upper triangle H[j][i] (j <= i) before L D L^T overwrites it, in a
+// fixed order (column i from the leaf, its diagonal first, then the rows toward the root) that
+// every grid form of the pair shares -- tau = C + h is then bit-identical across them.
+template <typename T, int N>
+RB_HD void fdh_hq(const T (&H)[N][N], const T (&av)[N], T (&h)[N]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) h[j] = T(0);
+#pragma unroll
+    for (int i = N - 1; i >= 0; --i) {
+        h[i] = fmadd(H[i][i], av[i], h[i]);
+#pragma unroll
+        for (int j = i - 1; j >= 0; --j) {
+            h[j] = fmadd(H[j][i], av[i], h[j]);
+            h[i] = fmadd(H[j][i], av[j], h[i]);
+        }
+    }
+}
+
 template <typename T, int N, bool FAST, typename LoadQdd, typename LoadTau, typename OutTau, typename OutQdd>
 RB_HD void fdh_idfd_eval(const T *mdl, const T (&qv)[N], const T (&qdv)[N], LoadQdd &&load_qdd, LoadTau &&load_tau,
                          OutTau &&out_tau, OutQdd &&out_qdd) {
-    T cs[N], sn[N], C[N], av[N], tv[N], tau[N], H[N][N], Di[N];
+    T cs[N], sn[N], C[N], av[N], tv[N], h[N], H[N][N], Di[N];
     InputGuard<T> gd;
     RB_STAGE("bias_fwd");
     fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C, gd);
     load_qdd(av);
-    InputGuard<T> gr = gd;  // tau: q, qd, qdd
-    gr.vals(av);
-#pragma unroll
-    for (int j = 0; j < N; ++j) tau[j] = C[j];
     reload_fence();
     RB_STAGE("crba");
     crba_core<T, N>(mdl, cs, sn, [&](int e, T v) {
         const int j = e % N, i = e / N;
-        if (j > i) return;  // the strictly-lower zeros
-        H[j][i] = v;
-        tau[j] = fmadd(v, av[i], tau[j]);
-        if (j < i) tau[i] = fmadd(v, av[j], tau[i]);
-        if (j == 0) out_tau(i, gr.out(tau[i]));
+        if (j <= i) H[j][i] = v;
     });
     load_tau(tv);
+    RB_STAGE("id");
+    fdh_hq<T, N>(H, av, h);
+    InputGuard<T> gr = gd;  // tau: q, qd, qdd
+    gr.vals(av);
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) out_tau(j, gr.out(C[j] + h[j]));
     RB_STAGE("ldl");
     fdh_ldl<T, N>(H, Di);
     InputGuard<T> gf = gd;  // qdd': q, qd, tau_in
@@ -211,6 +225,93 @@ __device__ __forceinline__ void idfd_lane(const T *mdl, const T *__restrict__ q,
     fdh_idfd_eval<T, N, FAST>(
         mdl, qv, qdv, [&](T (&v)[N]) { rows(qdd, v); }, [&](T (&v)[N]) { rows(tau_in, v); },
         [&](int j, T v) { st_row(tau, j * ld, off, v); }, [&](int j, T v) { st_row(qdd_out, j * ld, off, v); });
+}
+
+// The pair split over two waves (jit pack 5, small batches: at 2^17 configurations the
+// one-per-lane grid is 2 waves per SIMD and the launch time is one wave's ~1170-instruction
+// stream), as fdh_split_block1 below: per 64 configurations the bias wave evaluates C and the
+// q, qd checks and hands both over through LDS; its partner builds H, h = sym(H) qdd and
+// L D L^T, then after one block barrier stores tau = C + h and solves.  Same arithmetic as
+// idfd_lane (bit-identical outputs), ~620 / ~600 instructions per wave.
+template <typename T, int N, bool FAST>
+__device__ __forceinline__ void idfd_split_block1(const T *mdl, const T *__restrict__ q, const T *__restrict__ qd,
+                                                  const T *__restrict__ qdd, const T *__restrict__ tau_in,
+                                                  T *__restrict__ tau, T *__restrict__ qdd_out, uint32_t B,
+                                                  int64_t ld, int64_t bs) {
+    __shared__ T shC[2][N][64];
+    __shared__ float shG[2][64];  // the bias wave's running input check (InputGuard acc)
+    const uint32_t w = threadIdx.x >> 6, g = w & 1u, l = threadIdx.x & 63u;
+    const uint32_t tile = blockIdx.x >> 1, first = blockIdx.x * 128u;  // < B (grid ceil(B / 128))
+    const uint32_t c = ((blockIdx.x & 1u) << 7) + (g << 6) + l;       // within the tile
+    const uint32_t last = B - 1u - tile * 256u;
+    const bool live = first + (g << 6) + l < B;
+    const uint32_t off = (live ? c : last) * (uint32_t)sizeof(T);
+    const int64_t o = (int64_t)tile * bs;
+    if (w < 2) {
+        T qv[N], qdv[N], cs[N], sn[N], C[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+            qdv[j] = ld_row(qd + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        InputGuard<T> gd;
+        fdh_bias<T, N, FAST>(mdl, qv, qdv, cs, sn, C, gd);
+#pragma unroll
+        for (int j = 0; j < N; ++j) shC[g][j][l] = C[j];
+        shG[g][l] = gd.acc;
+        __syncthreads();
+    } else {
+        T qv[N], av[N], tv[N], cs[N], sn[N], C[N], h[N], H[N][N], Di[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            qv[j] = ld_row(q + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            av[j] = ld_row(qdd + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) sin_cos<FAST>(qv[j], sn[j], cs[j]);
+        crba_core<T, N>(mdl, cs, sn, [&](int e, T v) {
+            const int j = e % N, i = e / N;
+            if (j <= i) H[j][i] = v;
+        });
+        fdh_hq<T, N>(H, av, h);  // qdd's rows die here, before tau_in's land
+        InputGuard<T> gr;         // qdd here, q and qd from the bias wave below
+        gr.vals(av);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            tv[j] = ld_row(tau_in + o, j * ld, off);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        fdh_ldl<T, N>(H, Di);
+        // everything above feeds only the live-guarded stores: pinned, so the compiler cannot sink
+        // it past the barrier (fdh_split_block2)
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            asm volatile("" : "+v"(Di[j]));
+            asm volatile("" : "+v"(tv[j]));
+            asm volatile("" : "+v"(h[j]));
+        }
+        InputGuard<T> gf;
+        gf.vals(tv);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < N; ++j) C[j] = shC[g][j][l];
+        const float gb = shG[g][l];
+        gr.acc = guard_add(gr.acc, gb);
+        gf.acc = guard_add(gf.acc, gb);
+#pragma unroll
+        for (int j = N - 1; j >= 0; --j)
+            if (live) st_row(tau + o, j * ld, off, gr.out(C[j] + h[j]));
+        fdh_solve<T, N>(H, Di, tv, C, [&](int j, T v) {
+            if (live) st_row(qdd_out + o, j * ld, off, gf.out(v));
+        });
+    }
 }
 
 // Kinematic trees (Topo, tree_body.hip.hpp): the same definition with the tree forms of its

@@ -88,10 +88,12 @@ int jit_pack(JitKind kind, bool f64, int n) {
     // phases, mean 44.3-44.6).
     const int v = tuning().pack;
     if (kind == JitKind::Rollout) return ((v < 0 || v == 2 || v == 4) && !f64 && n <= 8) ? (v == 4 ? 4 : 2) : 1;
+    // the fused inverse + forward dynamics: one per lane, or its wave split (idfd_split_block1)
+    if (kind == JitKind::RneaFd) return v == 5 ? 5 : 1;
     if (kind != JitKind::Fd && kind != JitKind::Rnea) return 1;
     if (v == 3) return 3;
     if (v == 4) return (kind == JitKind::Fd && !f64) ? 4 : 1;  // split packed waves (fdh_split_block2)
-    if (v == 5) return (kind == JitKind::Fd && !f64) ? 5 : 1;  // split waves, one per lane (fdh_split_block1)
+    if (v == 5) return kind == JitKind::Fd ? 5 : 1;             // split waves, one per lane (fdh_split_block1)
     if (v >= 0) return (v >= 2 && !f64 && kind == JitKind::Fd) ? 2 : 1;
     if (kind == JitKind::Rnea) return (f64 && n <= 8) ? 3 : 1;
     return (!f64 && n <= 8) ? 2 : 1;
@@ -132,7 +134,8 @@ int jit_model_pack(const Model &m, JitKind kind, bool f64, int pack_req) {
     // 4 / 5 = the bias / mass-matrix wave split, packed / one per lane: fp32 mass-matrix FD only
     if (pack == 4 && kind == JitKind::Rollout && !(!f64 && jit_fd_form(m, kind) == 2 && !(tuning().jit_variant & 256)))
         return (!f64 && m.n <= 8) ? 2 : 1;  // the split needs the mass-matrix form: the pair instead
-    if ((pack == 4 || pack == 5) && kind != JitKind::Rollout && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2))
+    if (pack == 4 && kind != JitKind::Rollout && !(kind == JitKind::Fd && !f64 && jit_fd_form(m) == 2)) return 1;
+    if (pack == 5 && !((kind == JitKind::Fd || kind == JitKind::RneaFd) && jit_fd_form(m) == 2 && m.serial_revolute()))
         return 1;
     return pack;
 }
@@ -388,11 +391,15 @@ std::string jit_source(const Model &m, JitKind kind, bool f64, bool fast, int pa
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ qdd, const T *__restrict__ tau_in, T *__restrict__ tau, "
              "T *__restrict__ qdd_out, uint32_t B, int64_t ld, int64_t bs) {\n";
-        o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
-        o << "  if (b >= B) return;\n";
-        o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
-        o << "  rbamd::dev::idfd_lane<T, N, " << F
-          << ">(kModel, q + o, qd + o, qdd + o, tau_in + o, tau + o, qdd_out + o, threadIdx.x, ld);\n}\n";
+        if (pack == 5) {
+            o << "  rbamd::dev::idfd_split_block1<T, N, " << F << ">(kModel, q, qd, qdd, tau_in, tau, qdd_out, B, ld, bs);\n}\n";
+        } else {
+            o << "  const uint32_t b = blockIdx.x * 256u + threadIdx.x;\n";
+            o << "  if (b >= B) return;\n";
+            o << "  const int64_t o = (int64_t)blockIdx.x * bs;\n";
+            o << "  rbamd::dev::idfd_lane<T, N, " << F
+              << ">(kModel, q + o, qd + o, qdd + o, tau_in + o, tau + o, qdd_out + o, threadIdx.x, ld);\n}\n";
+        }
     } else if (kind == JitKind::Fd) {
         o << head << "rb_jit_kernel(const T *__restrict__ q, const T *__restrict__ qd, "
              "const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B, int64_t ld, int64_t bs) {\n";

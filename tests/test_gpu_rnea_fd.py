@@ -76,6 +76,32 @@ def test_rnea_fd_fr3_vs_oracle_and_separate_calls(ffi, dev, fr3_text, dt, B):
         assert (np.abs(res) / (1 + np.abs(h[3]))).max() <= 1e-8
 
 
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+@pytest.mark.parametrize("B", [100, 65536 - 3, 1 << 17])
+def test_rnea_fd_wave_split_bit_identical(ffi, dev, dt, B):
+    """The wave split (pack 5, idfd_split_block1: the fp32 default up to 2^16 configurations) and
+    the one-per-lane kernel (pack 1) run the same arithmetic: outputs equal bit for bit, both
+    layouts; ragged batches (lanes past B store nothing)."""
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    mb = ffi.Multibody.new()
+    assert mb.kernel_form("rnea_fd", dt == "f64", B) == (5 if dt == "f32" and B <= 65536 else 1)
+    x = _inputs(mb, B, 900 + B, np.float64 if dt == "f64" else np.float32)
+    xt = [_t(a, dev, tdt) for a in x]
+    try:
+        ffi.set_tuning("pack", 5)
+        assert mb.kernel_form("rnea_fd", dt == "f64", B) == 5
+        split = mb.rnea_fd_batch(*xt)
+        tt = [ffi.to_tiled(a) for a in xt]
+        split_t = [ffi.from_tiled(o, B) for o in mb.rnea_fd_batch_tiled(*tt, B)]
+        ffi.set_tuning("pack", 1)
+        assert mb.kernel_form("rnea_fd", dt == "f64", B) == 1
+        one = mb.rnea_fd_batch(*xt)
+    finally:
+        ffi.set_tuning("pack", -1)
+    for a, b, c in zip(split, split_t, one):
+        assert torch.equal(a, b) and torch.equal(a, c)
+
+
 def test_rnea_fd_shard_of_global_batch(ffi, dev):
     """Config 4: a 2^17 shard launched on its own equals those columns of the 2^20 launch, bit
     for bit (one lane body, any grid size)."""

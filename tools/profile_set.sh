@@ -8,7 +8,7 @@
 # failing step.
 #
 # usage (via gpurun): tools/profile_set.sh NAME...
-#   NAME in: clock rnea64 rnea32 rnea32s fd64 fd32 fd32s c30 c30_64 roll32 roll64
+#   NAME in: clock rnea64 rnea32 rnea32s fd64 idfd64 idfd64s fd32 fd32s c30 c30_64 roll32 roll64
 #            crba64 jac64 fk64 crba64t jac64t fk64t
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TRAFFIC_OUT=gpurun_out/traffic
@@ -18,7 +18,13 @@ summ() {  # TAG WORKLOAD
 }
 prof() {  # TAG WORKLOAD bench args...
   local tag=$1 wl=$2; shift 2
-  tools/profile_round.sh "$tag" "$@" && summ "$tag" "$wl"
+  # trace_check before summ deletes the per-dispatch trace: the traced run's own bench line against
+  # the mean of its last `steps` dispatches (the timed window) and the all-dispatch mean
+  tools/profile_round.sh "$tag" "$@" &&
+    mkdir -p "gpurun_out/sum/$tag" &&
+    python3 tools/trace_check.py "gpurun_out/${tag}_trace.log" "gpurun_out/$tag/trace" \
+      "gpurun_out/sum/$tag/trace_window.json" > /dev/null &&
+    summ "$tag" "$wl"
 }
 profany() {  # TAG WORKLOAD script args...
   local tag=$1 wl=$2; shift 2
@@ -33,6 +39,8 @@ one() {
     rnea32) prof rnea32 rnea_fr3_f32_tiled_b1048576 --kernel rnea --dtype f32 ;;
     rnea32s) prof rnea32s rnea_fr3_f32_tiled_b65536 --kernel rnea --dtype f32 --batch 65536 ;;
     fd64) prof fd64 fd_fr3_f64_tiled_b1048576 --kernel fd --dtype f64 ;;
+    idfd64) prof idfd64 rnea_fd_fr3_f64_tiled_b1048576 --kernel rnea_fd --dtype f64 ;;
+    idfd64s) prof idfd64s rnea_fd_fr3_f64_tiled_b131072 --kernel rnea_fd --dtype f64 --batch 131072 ;;
     fd32) prof fd32 fd_fr3_f32_tiled_b1048576 --kernel fd --dtype f32 ;;
     fd32s) prof fd32s fd_fr3_f32_tiled_b65536 --kernel fd --dtype f32 --batch 65536 ;;
     c30) prof c30 rnea_chain30_f32_tiled_b1048576 --kernel rnea --dtype f32 --dof 30 ;;

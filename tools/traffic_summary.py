@@ -54,7 +54,7 @@ def main():
     n = 7 if model == "fr3" else int(model[5:]) if model.startswith("chain") else 7
     B = int(workload.rsplit("_b", 1)[1])
     es = 4 if "_f32_" in workload else 8
-    alg = (8 if workload.startswith("rnea_fd") else 4) * n * es * B
+    alg = (6 if workload.startswith("rnea_fd") else 4) * n * es * B  # rnea_fd: q, qd, qdd, tau_in -> tau, qdd'
     q_rows = {"crba": n * n, "jac": 6 * n, "fwd": 3}.get(workload.split("_")[0])
     if q_rows is not None:  # q-only kernels: n rows read, n*n / 6n / 3 rows written
         alg = (n + q_rows) * es * B
