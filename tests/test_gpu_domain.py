@@ -7,14 +7,16 @@ batched entry point and every kernel form the launch policy can pick (hipRTC and
 generic; one per lane, packed pair, sequential pair, wave splits, parked long chain, ABA and
 mass-matrix forward dynamics, rollouts) to the oracle there:
 
-* large angles: q = +-M + U(-pi, pi) for M in 10 ... 1e6 rad, against the oracle at the usual
+* large angles: q = +-M + U(-pi, pi) for M in 10 ... 1e6 rad -- and up to the supported bound,
+  fp64 1e9, 1e12, 2^40 and 2^41 - 4 rad, fp32 2^22 - 4 rad -- against the oracle at the usual
   tolerances (fp64 1e-9 scaled; fp32 on the fp32-rounded inputs 1e-4 scaled for RNEA / CRBA,
   2e-5 n for fwd_kin / jac, the backward-error bound for forward dynamics -- the bounds of
   test_gpu_parity.py, unchanged);
 * a continuous-joint rollout whose angles cross 100 rad, against the oracle's step-by-step
   Euler, and its 2 pi k periodicity;
 * non-finite inputs: a configuration with a NaN or +-Inf anywhere among its inputs, or a joint
-  angle beyond the supported magnitude (2^45 rad fp64, 2^22 rad fp32), gets NaN in EVERY output
+  angle at or beyond the supported magnitude (2^41 rad fp64, 2^22 rad fp32: exactly the bound
+  and 1.5 x it), gets NaN in EVERY output
   (CRBA: every upper-triangle entry; the strictly-lower entries stay the ABI's exact zeros),
   and its neighbours -- including the other configuration of a paired lane -- are untouched.
   The reference yields NaN for every output that depends on the bad input (all of them for
@@ -34,7 +36,10 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 MAGS = [10.0, 100.0, 1e3, 1e4, 1e5, 1e6]
-LIMIT = {"f64": 2.0 ** 45, "f32": 2.0 ** 22}
+# the batched kernels' input domain (rigidbody_batch.h, spatial.hip.hpp InputGuard): |q| < LIMIT
+LIMIT = {"f64": 2.0 ** 41, "f32": 2.0 ** 22}
+# magnitudes beyond MAGS up to just below the bound (M + U(-pi, pi) < LIMIT)
+MAGS_HI = {"f64": [1e9, 1e12, 2.0 ** 40, 2.0 ** 41 - 4], "f32": [2.0 ** 22 - 4]}
 
 
 @pytest.fixture(scope="module")
@@ -147,15 +152,17 @@ def _check(kind, got, x, om, dt, n):
 
 @pytest.mark.parametrize("dt", ["f64", "f32"])
 def test_large_angles_every_form(dt, ffi, dev, fr3_text):
-    """FR3, every entry point and kernel form, |q| ~ 10 ... 1e6 rad, against the oracle."""
+    """FR3, every entry point and kernel form, |q| ~ 10 ... 1e6 rad and up to just below the
+    supported bound (MAGS_HI), against the oracle."""
     mb = ffi.Multibody.from_urdf_string(fr3_text)
     om = _oracle(fr3_text)
     lim = mb.limits()
     dtype = torch.float64 if dt == "f64" else torch.float32
     bad = []
     worst = {}
-    for mi, M in enumerate(MAGS):
+    for mi, M in enumerate(MAGS + MAGS_HI[dt]):
         x = _inputs(7, 2048 + 77, M, 1000 + mi, lim, dtype)
+        assert np.abs(x["q"]).max() < LIMIT[dt]
         xt = {k: _t(v, dev, dtype) for k, v in x.items()}
         for kind, form, tuning in FORMS[dt]:
             got = _run(ffi, mb, kind, xt, dtype, tuning)
@@ -253,9 +260,10 @@ def test_rollout_continuous_joints_past_100_rad(dt, ffi, dev, fr3_text):
 
 
 # ---------------------------------------------------------------- non-finite inputs
-def _poisoned(n, B, lim, dt, args, seed, poison=None):
+def _poisoned(n, B, lim, dt, args, seed, poison=None, boundary=True):
     """Inputs with one bad value per poisoned column: for each argument, joint and value in
-    (NaN, +Inf, -Inf, and for q +-1.5 x the supported magnitude), one column.  Returns the
+    (NaN, +Inf, -Inf, and for q +-1.5 x the supported magnitude and, with `boundary`, +-exactly
+    that magnitude), one column.  Returns the
     inputs and the poisoned column indices (all in the first 256-column block, so every
     paired-lane partner in the next block is clean)."""
     from rigidbody_amd import chains
@@ -266,7 +274,8 @@ def _poisoned(n, B, lim, dt, args, seed, poison=None):
     cols = []
     c = 0
     for k in poison or args:
-        vals = [np.nan, np.inf, -np.inf] + ([1.5 * LIMIT[dt], -1.5 * LIMIT[dt]] if k == "q" else [])
+        vals = [np.nan, np.inf, -np.inf] + ([1.5 * LIMIT[dt], -1.5 * LIMIT[dt]] if k == "q" else []) + \
+               ([LIMIT[dt], -LIMIT[dt]] if k == "q" and boundary else [])
         for j in range(n):
             for v in vals:
                 x[k][j, c] = v
@@ -324,7 +333,7 @@ def test_nonfinite_long_chain_and_rollout(dt, ffi, dev, fr3_text):
     mb30 = ffi.Multibody.from_urdf_string(xml)
     om30 = _oracle(xml)
     # 30 joints x 8 values: the q and qd columns fill the first block
-    x, cols = _poisoned(30, 1000, mb30.limits(), dt, ("q", "qd", "qdd"), 5000, poison=("q", "qd"))
+    x, cols = _poisoned(30, 1000, mb30.limits(), dt, ("q", "qd", "qdd"), 5000, poison=("q", "qd"), boundary=False)
     bad = []
     xt = {k: _t(v, dev, dtype) for k, v in x.items()}
     for form, tuning in (("auto", {}), ("unparked", {"rnea_park": 0})):
@@ -465,3 +474,59 @@ def test_trees_domain(case, dev):
                     assert (~np.isfinite(o[rows, col])).all(), (case, dtype, name, a, col)
             clean = [col for col in range(c, B)]
             assert np.isfinite(o[:, clean]).all(), (case, dtype, name)
+
+
+# ---------------------------------------------------------------- near-singular H, fp64
+# The fp64 forward dynamics near a singular mass matrix, judged by the bounds of a backward-stable
+# solve (L D L^T / Cholesky of an SPD matrix is normwise backward stable) rather than by a fixed
+# torque residual (rigidbody_batch.h "Accuracy"), with H_s = sym(H) and C = rnea(q, qd, 0) from
+# the oracle (multibody.rs:155-174 and :111-153 at qdd = 0):
+#   backward:  |H_s qdd - (tau - C)|_inf <= FD64_BACKWARD_K n eps64 (|H_s|_inf |qdd|_inf + |tau - C|_inf)
+#   forward:   |qdd - qdd_oracle|_inf <= FD64_FORWARD_K eps64 cond(H_s) (1 + |qdd_oracle|_inf)
+# (qdd_oracle: the oracle's fp64 Cholesky solve; its own backward ratio on this draw is 0.26 / n).
+# The torque residual through the RNEA is no judge here: at pitch -> +-pi/2 the solution grows
+# like cond(H) and the RNEA's own rounding of the cancelling link accelerations exceeds the fixed
+# 1e-8 (round 5: 1.08e-7 at ~1e3 rad offsets; the oracle's own solve fails it too).
+FD64_BACKWARD_K = 4.0
+FD64_FORWARD_K = 64.0
+
+
+def test_fd64_near_singular_floating_base(dev):
+    """The floating base's mass matrix is singular at pitch = +-pi/2 (the virtual joints' Euler
+    angles, rigidbody_batch.h RB_MODEL_FLOATING_BASE).  Pitch within 1e-3 ... 1e-6 of +-pi/2
+    (cond(H) 6e7 ... 1e14), every fp64 forward-dynamics form of the tree (the ABA default and the
+    mass-matrix form), against the two bounds above; the last quarter of the batch is the ordinary
+    draw (cond(H) < 1e4), held to the usual 1e-8 torque residual as well."""
+    import test_gpu_tree as tt
+    from rigidbody_amd import ffi
+
+    mb, om = tt._setup("floating14")
+    n = mb.n
+    B = 1024
+    q, qd, _, tau = tt._inputs(mb, B, 91)
+    rng = np.random.default_rng(92)
+    delta = 10.0 ** rng.uniform(-6, -3, B)
+    near = np.arange(B) < 3 * B // 4
+    q[4, near] = (rng.choice([-1.0, 1.0], B) * (math.pi / 2 - delta))[near]
+    H = om.crba_batch(q)
+    Hm = H.reshape(n, n, B).transpose(2, 1, 0)  # [b, row, col], upper triangle
+    Hs = np.triu(Hm) + np.triu(Hm, 1).transpose(0, 2, 1)
+    cond = np.linalg.cond(Hs)
+    assert cond[near].max() > 1e12 and cond[~near].max() < 1e4, (cond[near].max(), cond[~near].max())
+    ref = om.fd_batch(q, qd, tau)
+    y = tau - om.rnea_batch(q, qd, np.zeros_like(q))
+    eps = float(np.finfo(np.float64).eps)
+    normH = np.abs(Hs).sum(2).max(1)
+    worst = {}
+    for form, tuning in (("aba", {}), ("massmatrix", {"fd_form": 2})):
+        got = _tuned(ffi, tuning, lambda: mb.fd_batch(_t(q, dev), _t(qd, dev), _t(tau, dev))).cpu().numpy()
+        assert np.isfinite(got).all(), form
+        r = np.einsum("brc,cb->rb", Hs, got) - y
+        kb = (np.abs(r).max(0) / (n * eps * (normH * np.abs(got).max(0) + np.abs(y).max(0)))).max()
+        kf = (np.abs(got - ref).max(0) / (eps * cond * (1 + np.abs(ref).max(0)))).max()
+        res = om.rnea_batch(q[:, ~near], qd[:, ~near], got[:, ~near]) - tau[:, ~near]
+        worst[form] = (kb, kf)
+        assert kb <= FD64_BACKWARD_K, (form, "backward", kb)
+        assert kf <= FD64_FORWARD_K, (form, "forward", kf)
+        assert (np.abs(res) / (1 + np.abs(tau[:, ~near]))).max() <= 1e-8, form
+    print("near-singular floating base fp64 FD, (backward K, forward K):", worst, f"cond(H) max {cond.max():.2e}")
