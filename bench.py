@@ -415,14 +415,44 @@ def rollout_launcher(mb, B, dtype, K, dt=1e-3, seed=chains.SEED, reset=True, res
     ffi.fill_uniform(tau, lo * K, hi * K, seed + 2)  # list * K: the joints' ranges for every step row
     fn = getattr(ffi.lib(), f"multibody_rollout_batch_{'f32' if dtype == torch.float32 else 'f64'}")
     args = (mb.handle, q.data_ptr(), qd.data_ptr(), tau.data_ptr(), dt, K, None, B, B)
+    marks = []  # (start, end) hipEvent pairs around the kernel alone, when launch.mark is set
 
     def launch(i, sp):
         if reset:
             with _on_stream(sp):
                 state.copy_(init)
-        if not reset_only and fn(*args, sp):
+        if reset_only:
+            return
+        if launch.mark:
+            with _on_stream(sp):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                if fn(*args, sp):
+                    raise RuntimeError(ffi.last_error())
+                e1.record()
+            marks.append((e0, e1))
+        elif fn(*args, sp):
             raise RuntimeError(ffi.last_error())
 
+    def kernel_ms(n, warm=3):
+        """Mean device time of the rollout kernel alone over n reset + launch steps: an event pair
+        around each kernel (after its reset copy) on the launch stream."""
+        sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for i in range(warm):
+            launch(i, sp)
+        torch.cuda.synchronize()
+        marks.clear()
+        launch.mark = True
+        try:
+            for i in range(n):
+                launch(i, sp)
+            torch.cuda.synchronize()
+        finally:
+            launch.mark = False
+        return float(np.mean([a.elapsed_time(b) for a, b in marks]))
+
+    launch.mark = False
+    launch.kernel_ms = kernel_ms
     launch.keep = (q, qd, tau, init)
     return launch
 
@@ -573,14 +603,15 @@ def side_workloads(mb7, a):
         nl = budget_steps(rl, lo=100)
         w, lm = time_launches(rl, nl, 3, 1, 300.0)
         _, cm = time_launches(rollout_launcher(mb7, a.batch, dt, K, reset_only=True), nl, 3, 1, 0.0)
-        km = lm - cm
+        km = rl.kernel_ms(min(nl, 100))
         sec[f"rollout_fr3_{dn}_K16"] = {"steps_per_launch": K, "evals_per_s": a.batch * K * nl / w,
                                         "launches": nl, "launch_ms_avg": lm, "reset_ms_avg": cm,
                                         "kernel_ms_avg": km, "kernel_path": mb7.kernel_path("rollout", dn == "f64"),
                                         "note": ("evals = configurations x Euler steps; q, qd stay on chip (LDS); "
                                                  "every launch restarts from the initial state (a [2][n][B] device "
-                                                 "copy, reset_ms_avg, timed alone); evals_per_s includes it, "
-                                                 "kernel_ms_avg = launch_ms_avg - reset_ms_avg"),
+                                                 "copy, reset_ms_avg, timed alone); evals_per_s includes it; "
+                                                 "kernel_ms_avg = an event pair around each rollout kernel inside the "
+                                                 "reset + launch loop (the copy excluded), mean over launches"),
                                         "valu": valu_roofline(f"rollout_fr3_{dn}_K16_b{a.batch}", "rollout_step_fr3",
                                                               f"rollout_fr3_{dn}", dn, a.batch * K, km, dn == "f32"),
                                         "reference_formulation": reference_formulation("rollout_step_fr3", a.batch * K, km)}

@@ -63,8 +63,8 @@
  * Accuracy (tests/test_gpu_parity.py, test_gpu_domain.py, against the fp64 oracle).  fp64 RNEA,
  * CRBA, fwd_kin, jac: |d| <= 1e-9 (1 + |ref|) element-wise.  fp64 forward dynamics is a
  * backward-stable solve (L D L^T, or the ABA): with H_s = sym(H), C = rnea(q, qd, 0),
- *   |H_s qdd - (tau - C)|_inf <= 4 n eps64 (|H_s|_inf |qdd|_inf + |tau - C|_inf)
- *   |qdd - qdd_exact|_inf     <= 64 eps64 cond(H_s) (1 + |qdd_exact|_inf)
+ *   |H_s qdd - (tau - C)|_inf <= n eps64 (|H_s|_inf |qdd|_inf + |tau - C|_inf)
+ *   |qdd - qdd_exact|_inf     <= 4 eps64 cond(H_s) (1 + |qdd_exact|_inf)
  * -- at any conditioning (tested to cond(H) ~ 1e14, a floating base within 1e-6 rad of its pitch
  * singularity); for cond(H) <= ~1e4 (FR3 over its limits) that is a torque residual
  * |rnea(q, qd, qdd) - tau| <= 1e-8 (1 + |tau|).  fp32: RNEA 1e-4 (1 + |tau|) (chains past ~20
