@@ -170,3 +170,24 @@ def test_rnea_fd_other_models(ffi, dev, model):
         assert _scaled(tau.cpu().numpy(), tau_ref.cpu().numpy()) <= 1e-9
     else:
         assert torch.equal(tau, tau_ref)
+
+
+@pytest.mark.parametrize("name", ["fr3_golden.npz", "chain12_golden.npz", "chain30_golden.npz"])
+def test_rnea_fd_vs_golden(ffi, dev, fr3_text, name):
+    """The fused pair on the committed golden vectors (tools/gen_golden.py, oracle outputs): tau
+    against the golden RNEA torques at 1e-9 scaled, qdd_out against the golden CRBA-solve
+    accelerations at 1e-9 cond(H)/1e3 (test_gpu_parity.test_batched_f64_vs_golden's bound)."""
+    from conftest import load_npz
+    from test_gpu_parity import _model_xml
+
+    g = load_npz(name)
+    mb = ffi.Multibody.from_urdf_string(_model_xml(name, fr3_text))
+    n, B = g["q"].shape
+    tau, qdd2 = mb.rnea_fd_batch(*[_t(g[k], dev) for k in ("q", "qd", "qdd", "tau_in")])
+    assert _scaled(tau.cpu().numpy(), g["tau"]) <= 1e-9
+    q2 = qdd2.cpu().numpy()
+    for b in range(B):
+        Hb = g["H"][:, b].reshape(n, n).T
+        cond = np.linalg.cond(np.triu(Hb) + np.triu(Hb, 1).T)
+        err = np.abs(q2[:, b] - g["qdd_fd"][:, b]).max() / (1 + np.abs(g["qdd_fd"][:, b]).max())
+        assert err <= 1e-9 * max(1.0, cond / 1e3), (b, err, cond)
