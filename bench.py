@@ -916,7 +916,7 @@ def _summary(v):
     if "soa_us_median" in v:  # layout A/B
         return {"soa_us": _sig(v["soa_us_median"]), "tiled_us": _sig(v["tiled_us_median"])}
     out = {}
-    ms = v.get("kernel_ms_avg", v.get("step_ms_device", v.get("ms_per_step")))
+    ms = v.get("kernel_ms_avg", v.get("step_ms_device", v.get("kernel_ms_avg_max_rank", v.get("ms_per_step"))))
     if isinstance(ms, (int, float)):
         out["us"] = _sig(ms * 1e3)
     if isinstance(v.get("graph_ms_per_step_max_rank"), (int, float)):
@@ -927,9 +927,9 @@ def _summary(v):
     iv = (v.get("valu") or {}).get("issue_frac_held")
     if isinstance(iv, (int, float)):
         out["valu_frac"] = _sig(iv, 3)
-    for k in ("evals_per_s", "pairs_per_s"):
-        if k in v and "us" not in out:
-            out[k] = _sig(v[k])
+    for k in ("evals_per_s", "pairs_per_s", "graph_pairs_per_s"):
+        if isinstance(v.get(k), (int, float)) and ("us" not in out or "per_rank" in v):
+            out[k] = _sig(v[k])  # the N > 1 split lines: their whole-job rate too
     return out or None
 
 
