@@ -240,6 +240,11 @@ int multibody_rnea_fd_batch_tiled_f32(const Multibody *mb, const float *q, const
 int multibody_rnea_fd_batch_tiled_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
                                       const double *tau_in, double *tau, double *qdd_out, int64_t batch,
                                       void *stream);
+/* Blocking host-pointer form ([n][batch] host arrays in and out), as the *_batch_host_* below. */
+int multibody_rnea_fd_batch_host_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                     const double *tau_in, double *tau, double *qdd_out, int64_t batch);
+int multibody_rnea_fd_batch_host_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                     const float *tau_in, float *tau, float *qdd_out, int64_t batch);
 /* SoA [rows][ld] <-> tiled [ceil(batch/256)][rows][256] (to_tiled zero-fills the tail lanes). */
 int rb_to_tiled_f32(const float *src, int64_t ld, float *dst, int rows, int64_t batch, void *stream);
 int rb_to_tiled_f64(const double *src, int64_t ld, double *dst, int rows, int64_t batch, void *stream);

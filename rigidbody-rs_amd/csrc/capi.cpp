@@ -695,27 +695,31 @@ Multibody *new_from_text(const std::string &xml, unsigned flags = 0) {
 }  // namespace
 
 namespace {
+// nin input and nout output [n][batch] host arrays; launch(d_in, d_out, stream) gets the device
+// copies of the inputs (consecutive) and room for the outputs (consecutive).
 template <typename T, typename Launch>
-int host_batch(const Multibody *mb, const T *const *in, int nin, T *out, int64_t batch, Launch launch) {
+int host_batch(const Multibody *mb, const T *const *in, int nin, T *const *out, int nout, int64_t batch,
+               Launch launch) {
     int rc = check_batch(mb, batch, batch);
     if (rc) return rc;
     if (batch == 0) return RB_OK;
     for (int k = 0; k < nin; ++k)
         if (!in[k]) return set_err(RB_ERR_NULL, "NULL array");
-    if (!out) return set_err(RB_ERR_NULL, "NULL array");
+    for (int k = 0; k < nout; ++k)
+        if (!out[k]) return set_err(RB_ERR_NULL, "NULL array");
     const size_t per = (size_t)mb->model.n * (size_t)batch;
     T *d = nullptr;
     hipStream_t s = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_err(e, "hipStreamCreate");
-    e = hipMallocAsync((void **)&d, per * (nin + 1) * sizeof(T), s);
+    e = hipMallocAsync((void **)&d, per * (nin + nout) * sizeof(T), s);
     if (e != hipSuccess) { (void)hipStreamDestroy(s); return hip_err(e, "hipMallocAsync"); }
     for (int k = 0; k < nin && e == hipSuccess; ++k)
         e = hipMemcpyAsync(d + k * per, in[k], per * sizeof(T), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) rc = launch(d, d + nin * per, s);
     else rc = hip_err(e, "hipMemcpyAsync H2D");
-    if (rc == RB_OK) {
-        e = hipMemcpyAsync(out, d + nin * per, per * sizeof(T), hipMemcpyDeviceToHost, s);
+    for (int k = 0; k < nout && rc == RB_OK; ++k) {
+        e = hipMemcpyAsync(out[k], d + (nin + k) * per, per * sizeof(T), hipMemcpyDeviceToHost, s);
         if (e != hipSuccess) rc = hip_err(e, "hipMemcpyAsync D2H");
     }
     (void)hipFreeAsync(d, s);
@@ -729,7 +733,8 @@ int host_batch(const Multibody *mb, const T *const *in, int nin, T *out, int64_t
 template <typename T>
 int rnea_host(const Multibody *mb, const T *q, const T *qd, const T *qdd, T *tau, int64_t batch) {
     const T *in[3] = {q, qd, qdd};
-    return host_batch<T>(mb, in, 3, tau, batch, [&](T *d, T *o, hipStream_t s) {
+    T *out[1] = {tau};
+    return host_batch<T>(mb, in, 3, out, 1, batch, [&](T *d, T *o, hipStream_t s) {
         const size_t per = (size_t)mb->model.n * (size_t)batch;
         return rnea_batch<T>(mb, d, d + per, d + 2 * per, o, batch, batch, s);
     });
@@ -737,9 +742,20 @@ int rnea_host(const Multibody *mb, const T *q, const T *qd, const T *qdd, T *tau
 template <typename T>
 int fd_host(const Multibody *mb, const T *q, const T *qd, const T *tau, T *qdd, int64_t batch) {
     const T *in[3] = {q, qd, tau};
-    return host_batch<T>(mb, in, 3, qdd, batch, [&](T *d, T *o, hipStream_t s) {
+    T *out[1] = {qdd};
+    return host_batch<T>(mb, in, 3, out, 1, batch, [&](T *d, T *o, hipStream_t s) {
         const size_t per = (size_t)mb->model.n * (size_t)batch;
         return fd_batch<T>(mb, d, d + per, d + 2 * per, o, batch, batch, s);
+    });
+}
+template <typename T>
+int idfd_host(const Multibody *mb, const T *q, const T *qd, const T *qdd, const T *tau_in, T *tau, T *qdd_out,
+              int64_t batch) {
+    const T *in[4] = {q, qd, qdd, tau_in};
+    T *out[2] = {tau, qdd_out};
+    return host_batch<T>(mb, in, 4, out, 2, batch, [&](T *d, T *o, hipStream_t s) {
+        const size_t per = (size_t)mb->model.n * (size_t)batch;
+        return idfd_batch<T>(mb, d, d + per, d + 2 * per, d + 3 * per, o, o + per, batch, batch, s);
     });
 }
 }  // namespace
@@ -1238,6 +1254,14 @@ int multibody_rnea_batch_host_f64(const Multibody *mb, const double *q, const do
 int multibody_fd_batch_host_f64(const Multibody *mb, const double *q, const double *qd, const double *tau,
                                 double *qdd, int64_t batch) {
     return fd_host<double>(mb, q, qd, tau, qdd, batch);
+}
+int multibody_rnea_fd_batch_host_f64(const Multibody *mb, const double *q, const double *qd, const double *qdd,
+                                     const double *tau_in, double *tau, double *qdd_out, int64_t batch) {
+    return idfd_host<double>(mb, q, qd, qdd, tau_in, tau, qdd_out, batch);
+}
+int multibody_rnea_fd_batch_host_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
+                                     const float *tau_in, float *tau, float *qdd_out, int64_t batch) {
+    return idfd_host<float>(mb, q, qd, qdd, tau_in, tau, qdd_out, batch);
 }
 int multibody_rnea_batch_host_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
                                   float *tau, int64_t batch) {

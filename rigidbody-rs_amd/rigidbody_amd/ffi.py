@@ -106,6 +106,8 @@ for _t in ("f32", "f64"):
          [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_int, _vp, _i64, _i64, _vp])
 _sig("rb_set_tuning", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int])
 _sig("multibody_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _i64])
+_sig("multibody_rnea_fd_batch_host_f64", ctypes.c_int, [_vp, _dp, _dp, _dp, _dp, _dp, _dp, _i64])
+_sig("multibody_rnea_fd_batch_host_f32", ctypes.c_int, [_vp, _fp, _fp, _fp, _fp, _fp, _fp, _i64])
 for _t in ("f32", "f64"):
     _sig(f"multibody_rnea_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp])
     _sig(f"multibody_fd_batch_tiled_{_t}", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp])
@@ -578,6 +580,18 @@ class Multibody:
     def fd_batch_host(self, q, qd, tau, dtype=np.float64):
         """Blocking host form: multibody_fd_batch_host_f64 (default) or _f32 (dtype=np.float32)."""
         return self._host_call("fd", (q, qd, tau), dtype)
+
+    def rnea_fd_batch_host(self, q, qd, qdd, tau_in, dtype=np.float64):
+        """Blocking host form of rnea_fd_batch: (tau, qdd_out) as [n, B] numpy arrays
+        (multibody_rnea_fd_batch_host_f64, or _f32 with dtype=np.float32)."""
+        arrs = _host_soa((q, qd, qdd, tau_in), self.n, dtype)
+        B = arrs[0].shape[1]
+        outs = [np.empty_like(arrs[0]) for _ in range(2)]
+        f32 = arrs[0].dtype == np.float32
+        fn = getattr(_lib, f"multibody_rnea_fd_batch_host_{'f32' if f32 else 'f64'}")
+        ptr = _fp if f32 else _dp
+        _check(fn(self._h, *[a.ctypes.data_as(ptr) for a in arrs + outs], B), "rnea_fd_batch_host")
+        return outs[0], outs[1]
 
     def _host_call(self, kind, ins, dtype):
         arrs = _host_soa(ins, self.n, dtype)

@@ -191,3 +191,15 @@ def test_rnea_fd_vs_golden(ffi, dev, fr3_text, name):
         cond = np.linalg.cond(np.triu(Hb) + np.triu(Hb, 1).T)
         err = np.abs(q2[:, b] - g["qdd_fd"][:, b]).max() / (1 + np.abs(g["qdd_fd"][:, b]).max())
         assert err <= 1e-9 * max(1.0, cond / 1e3), (b, err, cond)
+
+
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_rnea_fd_host_pointers(ffi, dev, dt):
+    """multibody_rnea_fd_batch_host_*: the blocking host-pointer form equals the device form."""
+    mb = ffi.Multibody.new()
+    npd = np.float64 if dt == "f64" else np.float32
+    x = _inputs(mb, 3001, 55, npd)
+    tau_h, qdd_h = mb.rnea_fd_batch_host(*x, dtype=npd)
+    assert tau_h.dtype == npd and qdd_h.dtype == npd
+    tau_d, qdd_d = mb.rnea_fd_batch(*[_t(a, dev, torch.float64 if dt == "f64" else torch.float32) for a in x])
+    assert np.array_equal(tau_h, tau_d.cpu().numpy()) and np.array_equal(qdd_h, qdd_d.cpu().numpy())
