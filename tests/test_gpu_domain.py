@@ -62,6 +62,7 @@ FORMS = {
         ("rnea", "auto", {}), ("rnea", "one_per_lane", {"pack": 1}), ("rnea", "generic", {"jit": 0}),
         ("rnea_tiled", "auto", {}),
         ("fd", "massmatrix", {"fd_form": 2}), ("fd", "aba", {"fd_form": 1}),
+        ("fd", "split_one", {"fd_form": 2, "pack": 5}),
         ("fd", "aba_seqpair", {"fd_form": 1, "pack": 3}), ("fd", "generic", {"jit": 0}),
         ("fd_tiled", "auto", {}),
         ("crba", "auto", {}), ("crba", "generic", {"jit": 0}), ("crba_tiled", "auto", {}),
