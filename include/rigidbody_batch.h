@@ -48,8 +48,9 @@
  * arithmetic.  The batched kernels are exact (at the |q| <= pi tolerances of the tests) for
  *   every input finite (|x| < 2^1017 in fp64) and every revolute angle |q_j| < 2^41 rad
  *   (fp64) / 2^22 rad (fp32)
- * -- each sincos reduces the angle exactly over that range (spatial.hip.hpp; tested at
- * |q| up to 1e6 rad, tests/test_gpu_domain.py).  A configuration outside it -- a NaN or
+ * -- each sincos reduces the angle exactly over that range (spatial.hip.hpp; tested in every
+ * kernel form at |q| from 10 rad to just below the bound -- fp64 1e9, 1e12, 2^40, 2^41 - 4 --
+ * and at exactly the bound, tests/test_gpu_domain.py).  A configuration outside it -- a NaN or
  * +-Inf in any of its inputs, or an angle past the bound -- gets NaN in EVERY output (CRBA:
  * every upper-triangle entry; the strictly-lower entries stay the ABI's exact zeros), in
  * every kernel form; the other configurations of the batch, including the other half of a
