@@ -229,7 +229,8 @@ int multibody_fd_batch_tiled_f64(const Multibody *mb, const double *q, const dou
  * fp64), qdd_out with multibody_fd_batch_* bit for bit.  Other models run the two kernels
  * back to back on `stream`.  Input domain as above, per output: tau is NaN for a configuration
  * whose q, qd or qdd is out of the domain, qdd_out for one whose q, qd or tau_in is.  Outputs
- * must not overlap the inputs. */
+ * must not overlap the inputs or each other (an output passed as an input, e.g. tau_in as tau,
+ * is refused with RB_ERR_ARG). */
 int multibody_rnea_fd_batch_f32(const Multibody *mb, const float *q, const float *qd, const float *qdd,
                                 const float *tau_in, float *tau, float *qdd_out, int64_t batch, int64_t ld,
                                 void *stream);

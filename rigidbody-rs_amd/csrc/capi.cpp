@@ -623,6 +623,12 @@ int idfd_batch(const Multibody *mb, const T *q, const T *qd, const T *qdd, const
     if (rc) return rc;
     if (batch == 0) return RB_OK;
     if (!q || !qd || !qdd || !tau_in || !tau || !qdd_out) return set_err(RB_ERR_NULL, "NULL array");
+    // outputs must not overlap the inputs (the kernel reads tau_in after storing tau); the exact
+    // aliases a caller is likely to pass -- tau_in as tau, qdd as qdd_out -- are refused here
+    for (const T *o : {(const T *)tau, (const T *)qdd_out})
+        for (const T *i : {q, qd, qdd, tau_in})
+            if (o == i) return set_err(RB_ERR_ARG, "rnea_fd: an output array is also an input (no in-place form)");
+    if (tau == qdd_out) return set_err(RB_ERR_ARG, "rnea_fd: tau and qdd_out are the same array");
     const T *mdl = nullptr;
     if ((rc = device_consts<T>(mb, &mdl))) return rc;
     const int64_t per = tiled ? mb->model.n : 1;

@@ -203,3 +203,17 @@ def test_rnea_fd_host_pointers(ffi, dev, dt):
     assert tau_h.dtype == npd and qdd_h.dtype == npd
     tau_d, qdd_d = mb.rnea_fd_batch(*[_t(a, dev, torch.float64 if dt == "f64" else torch.float32) for a in x])
     assert np.array_equal(tau_h, tau_d.cpu().numpy()) and np.array_equal(qdd_h, qdd_d.cpu().numpy())
+
+
+def test_rnea_fd_refuses_aliased_outputs(ffi, dev):
+    """An output passed as an input (tau_in as tau, qdd as qdd_out) or both outputs the same
+    array: RB_ERR_ARG, nothing launched (rigidbody_batch.h)."""
+    mb = ffi.Multibody.new()
+    x = [_t(a, dev) for a in _inputs(mb, 300, 3)]
+    with pytest.raises(ffi.RigidBodyError, match="also an input"):
+        mb.rnea_fd_batch(*x, tau=x[3])
+    with pytest.raises(ffi.RigidBodyError, match="also an input"):
+        mb.rnea_fd_batch(*x, qdd_out=x[2])
+    o = torch.empty_like(x[0])
+    with pytest.raises(ffi.RigidBodyError, match="same array"):
+        mb.rnea_fd_batch(*x, tau=o, qdd_out=o)
