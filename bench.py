@@ -773,8 +773,8 @@ def _load_json(rel):
 
 def held_clock(name):
     """Median in-kernel shader clock (GHz) of kernel `name` under sustained load, from the
-    committed clock probe (tools/clock_probe.py, profiles/r05/clock_probe.jsonl), or None."""
-    path = os.path.join(REPO, "profiles", "r05", "clock_probe.jsonl")
+    committed clock probe (tools/clock_probe.py, profiles/r06/clock_probe.jsonl), or None."""
+    path = os.path.join(REPO, "profiles", "r06", "clock_probe.jsonl")
     if not os.path.exists(path):
         return None
     for ln in open(path):
@@ -816,7 +816,7 @@ def valu_roofline(workload, op_key, clock_key, dt_name, evals, kern_ms, packed):
         clk = held_clock(clock_key)
         if clk:
             out.update({"held_clock_ghz": clk, "issue_frac_held": busy / (clk * 1e9 * t),
-                        "clock_source": f"profiles/r05/clock_probe.jsonl [{clock_key}]"})
+                        "clock_source": f"profiles/r06/clock_probe.jsonl [{clock_key}]"})
         fl = tr.get("valu_flops_per_launch", {})
         # the SQ_INSTS_VALU_FLOPS_* counters count per wave-instruction (an FMA 2, a packed FMA 4):
         # x 64 lanes for the FLOPs executed, as rocprof-compute's VALU FLOP metric
