@@ -121,19 +121,31 @@ def test_rnea_fd_shard_of_global_batch(ffi, dev):
     assert torch.isfinite(tau).all() and torch.isfinite(qdd2).all()
 
 
+@pytest.mark.parametrize("pack", [1, 5])
 @pytest.mark.parametrize("dt", ["f64", "f32"])
-def test_rnea_fd_input_domain_per_output(ffi, dev, dt):
+def test_rnea_fd_input_domain_per_output(ffi, dev, dt, pack):
     """tau is NaN exactly for configurations whose q, qd or qdd is out of the domain; qdd_out
-    exactly for those whose q, qd or tau_in is (rigidbody_batch.h); neighbours untouched."""
+    exactly for those whose q, qd or tau_in is (rigidbody_batch.h); neighbours untouched -- one
+    per lane and the wave split (whose bias wave hands its q, qd check over in LDS)."""
     tdt = torch.float64 if dt == "f64" else torch.float32
     mb = ffi.Multibody.new()
+    ffi.set_tuning("pack", pack)
+    try:
+        assert mb.kernel_form("rnea_fd", dt == "f64", 512) == pack
+        _domain_case(ffi, mb, dev, dt, tdt)
+    finally:
+        ffi.set_tuning("pack", -1)
+
+
+def _domain_case(ffi, mb, dev, dt, tdt):
     B = 512
     x = _inputs(mb, B, 77, np.float64 if dt == "f64" else np.float32)
     lim_angle = 2.0 ** 41 if dt == "f64" else 2.0 ** 22
     bad = {  # column -> (input index, joint, value)
         10: (0, 0, np.nan), 11: (0, 3, lim_angle * 1.5), 12: (1, 6, np.inf), 13: (2, 2, np.nan),
-        14: (2, 0, -np.inf), 15: (3, 4, np.nan), 16: (3, 1, np.inf),
+        14: (2, 0, -np.inf), 15: (3, 4, np.nan), 16: (3, 1, np.inf), 17: (0, 5, -lim_angle),
     }
+    x[0][2, 18] = lim_angle - 4.0  # just inside the domain: finite outputs
     for c, (k, j, v) in bad.items():
         x[k][j, c] = v
     xt = [_t(a, dev, tdt) for a in x]
