@@ -283,12 +283,10 @@ hipError_t no_generic(const Multibody *mb) {
 constexpr uint32_t kPackMinBatch = 1u << 18;
 // fp32 mass-matrix forward dynamics at small batches: one wave per SIMD at most, so the launch
 // time follows each wave's instruction stream; the wave splits (fdh_body.hip.hpp) halve it.
-// Up to 2^15 configurations the one-per-lane split (pack 5: B/32 waves), up to 2^17 the
-// packed split (pack 4: B/64 waves; the rollout's split takes the same bound), above it the
-// packed pair.  FR3, HIP graph:
-// 32768 3.42 us (pack 5) / 3.77 (4) / 4.08 (one per lane); 65536 4.03 (4) / 4.30 (5) / 4.28 (1);
-// 131072 5.30 (4) / 5.37 (pair) / 5.62 (5) (profiles/r03/split/).
-constexpr uint32_t kSplit1MaxBatch = 1u << 15;
+// Up to 2^17 configurations the one-per-lane split (pack 5: B/32 waves, its roles alternating
+// over the SIMDs), above it the packed pair; the packed split (pack 4: B/64 waves) is the
+// rollout's, with the same bound.  FR3, HIP graph (profiles/r06/mix/): 32768 3.53 us (pack 5)
+// / 3.99 (4); 65536 4.15 (5) / 4.24 (4); 131072 5.45 (5) / 5.50 (4).
 constexpr uint32_t kSplitMaxBatch = 1u << 17;
 
 // The forward-dynamics kernel a launch of B configurations takes (auto policy when the
@@ -298,7 +296,7 @@ int fd_pack(const Multibody *mb, bool f64, uint32_t B) {
     if (rbamd::tuning().pack < 0) {
         if (!f64 && rbamd::jit_fd_form(mb->model) == 2 && mb->model.n <= 8 &&
             mb->model.serial_revolute())  // splits: serial chains, measured on FR3
-            pack = B <= kSplit1MaxBatch ? 5 : B <= kSplitMaxBatch ? 4 : 0;
+            pack = B <= kSplitMaxBatch ? 5 : 0;
         else  // paired lanes halve the grid: below kPackMinBatch one per lane fills more CUs
             pack = B < kPackMinBatch ? 1 : 0;
     }

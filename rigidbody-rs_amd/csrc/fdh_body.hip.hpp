@@ -240,7 +240,9 @@ __device__ __forceinline__ void idfd_split_block1(const T *mdl, const T *__restr
                                                   int64_t ld, int64_t bs) {
     __shared__ T shC[2][N][64];
     __shared__ float shG[2][64];  // the bias wave's running input check (InputGuard acc)
-    const uint32_t w = threadIdx.x >> 6, g = w & 1u, l = threadIdx.x & 63u;
+    const uint32_t wr = threadIdx.x >> 6;  // roles alternate as in fdh_split_block1
+    const uint32_t w = (((wr ^ blockIdx.x) & 1u) << 1) + (wr >> 1);
+    const uint32_t g = w & 1u, l = threadIdx.x & 63u;
     const uint32_t tile = blockIdx.x >> 1, first = blockIdx.x * 128u;  // < B (grid ceil(B / 128))
     const uint32_t c = ((blockIdx.x & 1u) << 7) + (g << 6) + l;       // within the tile
     const uint32_t last = B - 1u - tile * 256u;
@@ -410,8 +412,8 @@ __device__ __forceinline__ void fdh_lane2(const f2 *mdl, const float *__restrict
         [&](int j, f2 v) { st_row2(qdd, j * ld, offA, offB, v); });
 }
 
-// Small batches on packed lanes (jit pack 4, fp32; capi.cpp jit_fd takes it from 2^15 to 2^17
-// configurations).  There the one-per-lane grid is at most one wave per SIMD and the kernel
+// Small batches on packed lanes (jit pack 4, fp32; the rollout's split, and fp32 FD by tuning
+// -- capi.cpp fd_pack takes pack 5 up to 2^17 configurations).  There the one-per-lane grid is at most one wave per SIMD and the kernel
 // time is the load burst plus ONE wave's dependent instruction stream (~1120 VALU at 65536);
 // the packed pair halves the instructions per configuration but, at two configurations per
 // lane, leaves half the SIMDs without a wave.  Here each pair of packed waves splits the work
@@ -486,8 +488,8 @@ __device__ __forceinline__ void fdh_split_block2(const f2 *mdl, const float *__r
     }
 }
 
-// The same split one configuration per lane (jit pack 5; capi.cpp jit_fd takes it up to 2^15
-// configurations, where it keeps one wave per SIMD that the packed split would leave idle): a
+// The same split one configuration per lane (jit pack 5; capi.cpp fd_pack takes it up to 2^17
+// configurations, where it keeps every SIMD busy that the packed split would leave idle): a
 // 256-thread block covers 128 configurations -- half a 256-configuration tile -- with two wave
 // pairs (waves 0/2 and 1/3: configurations [0,64) and [64,128) of that half).  FR3 fp32 32768:
 // 3.42 us vs 3.77 packed split, 4.08 one per lane (HIP graph).  fp64 measured slower at every
@@ -497,7 +499,13 @@ __device__ __forceinline__ void fdh_split_block1(const T *mdl, const T *__restri
                                                  const T *__restrict__ tau, T *__restrict__ qdd, uint32_t B,
                                                  int64_t ld, int64_t bs) {
     __shared__ T shC[2][N][64];
-    const uint32_t w = threadIdx.x >> 6, g = w & 1u, l = threadIdx.x & 63u;
+    // The roles alternate by wave and block parity (w is a permutation of the wave index), so
+    // the two blocks a CU holds put a bias wave and a mass-matrix wave on each SIMD rather than
+    // two of one kind: FR3 fp32, HIP graph, 65536 4.15 vs 4.21 us, 131072 5.45 vs 5.53
+    // (profiles/r06/mix/).
+    const uint32_t wr = threadIdx.x >> 6;
+    const uint32_t w = (((wr ^ blockIdx.x) & 1u) << 1) + (wr >> 1);
+    const uint32_t g = w & 1u, l = threadIdx.x & 63u;
     const uint32_t tile = blockIdx.x >> 1, first = blockIdx.x * 128u;  // < B (grid ceil(B / 128))
     const uint32_t c = ((blockIdx.x & 1u) << 7) + (g << 6) + l;       // within the tile
     const uint32_t last = B - 1u - tile * 256u;

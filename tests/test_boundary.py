@@ -293,8 +293,8 @@ def test_jit_kernel_forms_compile(ffi, fr3_text):
     assert "#define RB_NT 3" in mb.jit_source(False, "rnea", batch=1 << 20, tiled=False)
     assert "rnea_lane_seq2<" not in mb.jit_source(True, "rnea", batch=1 << 17)
     assert "fdh_split_block1<" in mb.jit_source(False, "fd", batch=1 << 15)
-    assert "fdh_split_block2<" in mb.jit_source(False, "fd", batch=65536)
-    assert "fdh_split_block2<" in mb.jit_source(False, "fd", batch=1 << 17)
+    assert "fdh_split_block1<" in mb.jit_source(False, "fd", batch=65536)
+    assert "fdh_split_block1<" in mb.jit_source(False, "fd", batch=1 << 17)
     assert "fdh_lane2<" in mb.jit_source(False, "fd", batch=(1 << 17) + 1)
     assert "rollout_split_block2<" in mb.jit_source(False, "rollout", batch=65536)
     assert mb.jit_compile(f64=True, kind="rnea", batch=1 << 20, tiled=True) > 1000

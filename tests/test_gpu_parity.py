@@ -448,7 +448,7 @@ def test_cpp_batch_consumer(dev):
 
     exe = os.path.join(PKG, "bin", "batch_bench")
     assert os.path.exists(exe), "make -C rigidbody-rs_amd bin/batch_bench"
-    for kind, dt, B, layout, form in (("rnea", "f32", 65536, "tiled", 1), ("fd", "f32", 65536, "tiled", 4),
+    for kind, dt, B, layout, form in (("rnea", "f32", 65536, "tiled", 1), ("fd", "f32", 65536, "tiled", 5),
                                       ("fd", "f64", 1000, "soa", 1), ("rnea", "f64", 300007, "tiled", 1)):
         r = subprocess.run([exe, kind, dt, str(B), "200", layout], capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, r.stderr[-2000:]
@@ -461,7 +461,7 @@ def test_cpp_batch_consumer(dev):
 
 def test_small_batch_fd_forms_strided(ffi, dev, fr3_text):
     """The small-batch forward-dynamics forms (policy: the one-per-lane wave split, pack 5, up to
-    2^15; the packed wave split, pack 4) and the paired / one-per-lane forms through [7, ld]
+    2^17; the packed wave split, pack 4, by tuning) and the paired / one-per-lane forms through [7, ld]
     buffers with ld > B: padding columns untouched, every form within the fp32 backward-error
     bound of the oracle's CRBA solve, the policy's launch bit-identical to
     pack 5."""
@@ -845,8 +845,8 @@ def test_fd_forms_vs_oracle(dt, ffi, dev, fr3_text):
 
 def test_policy_forms_at_config_sizes(ffi, dev, fr3_text):
     """The auto policy's kernel at each BASELINE config size is the form the oracle tests force,
-    bit for bit: fp32 forward dynamics at 65536 / 65539 (config 3) takes the packed wave split
-    (pack 4, fdh_split_block2) and at 2^20 the packed pair (2); at config 4's 2^17 fp64 shard the
+    bit for bit: fp32 forward dynamics at 65536 / 65539 (config 3) takes the one-per-lane wave
+    split (pack 5, fdh_split_block1) and at 2^20 the packed pair (2); at config 4's 2^17 fp64 shard the
     RNEA and the forward dynamics take one configuration per lane (1) -- each compared with the
     same launch under the forced form (multibody.rs:111-174 through test_fd_forms_vs_oracle /
     test_batched_*_vs_golden)."""
@@ -854,7 +854,7 @@ def test_policy_forms_at_config_sizes(ffi, dev, fr3_text):
 
     mb = ffi.Multibody.from_urdf_string(fr3_text)
     lim = mb.limits()
-    cases = [("fd", "f32", 65536, 4), ("fd", "f32", 65539, 4), ("fd", "f32", 1 << 20, 2),
+    cases = [("fd", "f32", 65536, 5), ("fd", "f32", 65539, 5), ("fd", "f32", 1 << 20, 2),
              ("fd", "f64", 1 << 17, 1), ("rnea", "f64", 1 << 17, 1), ("rnea", "f32", 65536, 1)]
     for kind, dt, B, form in cases:
         f64 = dt == "f64"
@@ -880,7 +880,7 @@ def test_fd32_forms_bit_identical(ffi, dev, fr3_text):
     """Every launch form of the fp32 mass-matrix forward dynamics (one per lane, packed pair,
     packed / one-per-lane wave splits) runs the same fdh_bias / fdh_factor / fdh_solve code, so
     the result does not depend on the form -- i.e. on the batch size or shard a configuration
-    lands in (the policy switches form at 2^15 / 2^17)."""
+    lands in (the policy switches form at 2^17)."""
     from rigidbody_amd import chains
 
     mb = ffi.Multibody.from_urdf_string(fr3_text)
