@@ -148,7 +148,8 @@ std::string jit_tag(JitKind kind, bool f64, int n) {
            ":t" + std::to_string(jit_f64_tab(f64) ? 1 : 0) + ":r" + std::to_string(tuning().split_rot) + ":v" +
            std::to_string(tuning().jit_variant) + ":f" + std::to_string(tuning().fd_form) + ":k" +
            std::to_string(kind == JitKind::Rnea ? tuning().rnea_park.load() : 0) + ":e" +
-           std::to_string(kind == JitKind::Rnea ? tuning().rnea_rev.load() : 0);
+           std::to_string(kind == JitKind::Rnea ? tuning().rnea_rev.load() : 0) + ":a" +
+           std::to_string(tuning().kernarg_preload.load());
 }
 
 int code_vgprs(const std::vector<char> &code) {
@@ -489,6 +490,12 @@ bool rtc_compile(const std::string &src, const std::string &arch, bool no_licm, 
     if (no_licm) {
         optv.push_back("-mllvm");
         optv.push_back("-disable-machine-licm");
+    }
+    const int preload = tuning().kernarg_preload;
+    const std::string preload_opt = "-amdgpu-kernarg-preload-count=" + std::to_string(preload);
+    if (preload > 0) {
+        optv.push_back("-mllvm");
+        optv.push_back(preload_opt.c_str());
     }
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)optv.size(), optv.data());
     if (rc != HIPRTC_SUCCESS) {

@@ -75,7 +75,8 @@ int jit_seq_tail(bool tiled);
 // cliff: a kernel built without an occupancy target that lands just past 256 registers (one
 // wave per SIMD, <= 16 over) is rebuilt with a 2-wave target -- a few spilled values cost less
 // than half the SIMD's waves (the 9-joint tree's fp64 RNEA: 258 registers; 65.0 vs 92.9 us at
-// 2^20 with 12 B of scratch).
+// 2^20 with 12 B of scratch; 234 registers at the first build once the kernel arguments are
+// preloaded, tuning.hpp kernarg_preload).
 // final_src (optional): the source of the code object returned -- the occupancy-cliff rebuild's
 // when that rule applied (multibody_jit_source_ex reports this one).
 bool jit_compile(const Model &m, JitKind kind, bool f64, bool fast, const std::string &arch,

@@ -51,6 +51,7 @@ const Key kKeys[] = {
     {"seq_tail", &Tuning::seq_tail, true},
     {"kin_jit", &Tuning::kin_jit, true},
     {"kin_nt", &Tuning::kin_nt, true},
+    {"kernarg_preload", &Tuning::kernarg_preload, true},
 };
 
 // RB_<KEY> environment overrides (upper-cased key), experimental ones only with RB_EXPERIMENTAL=1.

@@ -96,6 +96,13 @@ struct Tuning {
     // jac 70.3 vs 89.3, fp32 CRBA 40.5 vs 46.2 -- at the no-math probe's 5.9 TB/s for these row
     // shapes), 3 for fwd_kin (16.4 vs 17.2 with stores only, 18.3 with neither).
     std::atomic<int> kin_nt{-1};
+    // JIT kernels: the first `kernarg_preload` dwords of the kernel arguments arrive in SGPRs
+    // with the dispatch (-amdgpu-kernarg-preload-count; 14 = every user SGPR the kernarg pointer
+    // leaves) instead of by scalar loads at entry -- the code object keeps a 256-byte prologue
+    // that loads them for firmware without preload.  0 = off.  Interleaved A/B, HIP graph, two
+    // boxes (profiles/r06/ab/ab_*_preload.log): RNEA fp32 65536 3.58-3.60 vs 3.62-3.65 us, FD fp32
+    // 65536 4.11-4.13 vs 4.16-4.18; the fused fp64 2^17 shard and the headline within noise.
+    std::atomic<int> kernarg_preload{14};
 };
 
 // Process-wide knobs, initialised from RB_JIT / RB_PACK / RB_RNEA_STREAM (and, with

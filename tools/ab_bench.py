@@ -65,7 +65,7 @@ def main():
     # every knob any variant sets is reset to the library default (tuning.hpp) before each
     # variant, so a knob of one variant never leaks into the next
     defaults = {"rnea_stream": -1, "grid_factor": 1, "jit": 1, "rnea_nt": -1, "fd_nt": 3, "jit_waves": -1,
-                "opaque_consts": -1, "pack": -1, "f64_tab": -1, "split_rot": -1, "jit_variant": 0, "seq_tail": -1, "kin_jit": -1, "kin_nt": -1, "rnea_park": -1, "rnea_rev": -1,
+                "opaque_consts": -1, "pack": -1, "f64_tab": -1, "split_rot": -1, "jit_variant": 0, "seq_tail": -1, "kin_jit": -1, "kin_nt": -1, "rnea_park": -1, "rnea_rev": -1, "kernarg_preload": 14,
                 "fd_form": -1}
     used = {kv.split("=")[0] for v in a.variants for kv in v.split(",")} - {"streams"}
     keys = [(v, lp) for v in a.variants for lp in launches]
