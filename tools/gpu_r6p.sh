@@ -1,5 +1,6 @@
-#!/bin/bash
-# Round 6: raised wave priority while a lane issues its rows (RB_VARIANT bit 262144), headline
+# round 6: non-temporal load / store bits of the fused pair (fd_nt: 1 loads, 2 stores)
 set -o pipefail
 mkdir -p gpurun_out/r6p
-timeout -k 10 400 python tools/ab_bench.py --kernel rnea --dtype f64 --batch 1048576 --layouts tiled --rounds 9 --steps 100 --variants jit_variant=0 jit_variant=262144 jit_variant=262144,jit_waves=4 > gpurun_out/r6p/ab_rnea64_prio.log 2>&1 || exit 1
+V="fd_nt=3 fd_nt=2 fd_nt=1 fd_nt=0"
+timeout -k 10 240 python tools/ab_bench.py --kernel rnea_fd --dtype f64 --batch 131072 --graph --layouts tiled --rounds 7 --steps 300 --variants $V > gpurun_out/r6p/ab_idfd64s_nt.log 2>&1 || exit 1
+timeout -k 10 240 python tools/ab_bench.py --kernel rnea_fd --dtype f64 --layouts tiled --rounds 7 --steps 200 --variants $V > gpurun_out/r6p/ab_idfd64_nt.log 2>&1 || exit 1
