@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 6: the 30-link fp32 RNEA (config 5) -- the reversed sweep (rnea_rev = 2, 5 waves/SIMD,
+# (the A/B selector was removed after this run, DESIGN.md §10: rejected)
 # +27% VALU) against the parked form (3 waves/SIMD)
 set -o pipefail
 mkdir -p gpurun_out/r6x
