@@ -395,6 +395,8 @@ hipError_t launch_fd_any(const Multibody *mb, const T *mdl, const T *q, const T 
 // 131072 6.79 vs 6.49; fp64 65536 6.64 vs 6.70, 131072 11.55 vs 10.67, 262144 22.06 vs 20.59 --
 // as for the forward dynamics alone (fp64 FD split 10.16 vs 8.62 us at 2^17): the SIMDs already
 // hold 2 waves of the one-per-lane kernel there, and the split repeats the loads and sincos.
+// With the split's roles alternating over the SIMDs (round 6, profiles/r06/mix/): fp32 65536
+// 4.75 us, 131072 6.53 vs 6.46 one per lane -- the bound stays.
 constexpr uint32_t kIdfdSplitMaxBatch32 = 1u << 16;
 int idfd_pack(bool f64, uint32_t B) {
     if (rbamd::tuning().pack >= 0) return 0;
